@@ -1,0 +1,309 @@
+// api.hip — the C ABI (include/honu_codec.h) over the gfx950 kernels.
+//
+// One context per device: it owns the only allocations the library makes
+// (per-record decode scratch, count/offset columns and scan partials), sized
+// once for a maximum batch so that every codec call is allocation- and
+// sync-free and can be captured into a hipGraph.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "kernels.h"
+
+using namespace honu;
+
+struct honu_ctx {
+    int device;
+    uint64_t max_n;
+    LaunchGeom geom;
+    void *ws;
+    uint64_t *counts;        // 3 * max_n
+    uint64_t *offs;          // 3 * max_n
+    uint64_t *totals;        // 4
+    uint64_t *partials;      // scan partials
+    DecodeScratch *scratch;  // max_n
+};
+
+static thread_local char g_last_error[256];
+
+static int32_t hip_fail(hipError_t e, const char *what) {
+    snprintf(g_last_error, sizeof g_last_error, "%s: %s", what, hipGetErrorString(e));
+    return HONU_E_HIP;
+}
+#define HIPCHK(x)                                  \
+    do {                                           \
+        hipError_t e_ = (x);                       \
+        if (e_ != hipSuccess) return hip_fail(e_, #x); \
+    } while (0)
+
+static int32_t arg_fail(const char *what) {
+    snprintf(g_last_error, sizeof g_last_error, "invalid argument: %s", what);
+    return HONU_E_ARG;
+}
+
+static bool aligned(const void *p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
+
+static int env_int(const char *name, int dflt) {
+    const char *v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+
+extern "C" {
+
+uint32_t honu_abi_version(void) { return HONU_ABI_VERSION; }
+uint64_t honu_sizeof_meta(void) { return sizeof(honu_meta); }
+uint64_t honu_sizeof_acl(void) { return sizeof(honu_acl); }
+uint64_t honu_sizeof_record_info(void) { return sizeof(honu_record_info); }
+const char *honu_last_error(void) { return g_last_error; }
+
+const char *honu_status_string(int32_t st) {
+    switch (st) {
+    case HONU_OK: return "ok";
+    case HONU_ERR_BAD_VERSION: return "object is malformed: cannot decode specified version";
+    case HONU_ERR_MALFORMED: return "object is malformed: cannot parse data or metadata";
+    case HONU_ERR_EOF: return "EOF";
+    case HONU_ERR_UNEXPECTED_EOF: return "unexpected EOF";
+    case HONU_ERR_NO_LENGTH: return "field not written with length value";
+    case HONU_ERR_PARSE_BOOLEAN: return "could not parse boolean value";
+    case HONU_ERR_PARSE_VARINT: return "could not parse varint";
+    case HONU_ERR_PANIC: return "input on which the Go reference panics";
+    case HONU_ERR_CAPACITY: return "output capacity exceeded";
+    case HONU_ERR_INPUT: return "input span or list outside its arena";
+    case HONU_E_ARG: return "invalid argument";
+    case HONU_E_WORKSPACE: return "batch larger than the context's reserved records";
+    case HONU_E_HIP: return "HIP runtime error";
+    case HONU_E_NO_DEVICE: return "no gfx950 device";
+    default: return "unknown status";
+    }
+}
+
+honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
+    int32_t dummy;
+    if (!err) err = &dummy;
+    *err = HONU_OK;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) {
+        snprintf(g_last_error, sizeof g_last_error, "no HIP device %d (count %d)", device, count);
+        *err = HONU_E_NO_DEVICE;
+        return nullptr;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess ||
+        strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        snprintf(g_last_error, sizeof g_last_error, "device %d is %s, this build targets gfx950",
+                 device, prop.gcnArchName);
+        *err = HONU_E_NO_DEVICE;
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        *err = HONU_E_HIP;
+        return nullptr;
+    }
+    honu_ctx *c = (honu_ctx *)calloc(1, sizeof(honu_ctx));
+    c->device = device;
+    c->max_n = max_records ? max_records : 1;
+    c->geom.num_cu = prop.multiProcessorCount;
+    c->geom.per_record_blocks = env_int("HONU_RECORD_BLOCKS", prop.multiProcessorCount * 8);
+    c->geom.copy_blocks = env_int("HONU_COPY_BLOCKS", prop.multiProcessorCount * 4);
+    const uint64_t n = c->max_n;
+    const uint64_t np = scan_partials_len(n, 3) + scan_partials_len(n, 1);
+    const uint64_t bytes = 8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 256;
+    if (hipMalloc(&c->ws, bytes) != hipSuccess) {
+        snprintf(g_last_error, sizeof g_last_error, "hipMalloc(%llu) failed",
+                 (unsigned long long)bytes);
+        free(c);
+        *err = HONU_E_HIP;
+        return nullptr;
+    }
+    uint64_t *w = (uint64_t *)c->ws;
+    c->counts = w;
+    w += 3 * n;
+    c->offs = w;
+    w += 3 * n;
+    c->totals = w;
+    w += 4;
+    c->partials = w;
+    w += np;
+    c->scratch = (DecodeScratch *)w;
+    return c;
+}
+
+void honu_ctx_destroy(honu_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipFree(ctx->ws);
+    free(ctx);
+}
+
+uint64_t honu_ctx_max_records(const honu_ctx *ctx) { return ctx ? ctx->max_n : 0; }
+
+// ---------------------------------------------------------------------------
+// encode
+// ---------------------------------------------------------------------------
+int32_t honu_encode_sizes(honu_ctx *ctx, const honu_meta *d_meta, uint64_t var_len,
+                          const honu_acl *d_acl, uint64_t acl_len, const uint32_t *d_regions,
+                          uint64_t regions_len, const uint64_t *d_payload_off, uint64_t n,
+                          uint64_t *d_sizes, int32_t *d_status, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n && (!d_meta || !d_payload_off || !d_sizes)) return arg_fail("null pointer");
+    if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_encode_sizes(ctx->geom, d_meta, var_len, d_acl, acl_len, d_regions, regions_len,
+                               d_payload_off, n, d_sizes, d_status, (hipStream_t)stream));
+    return HONU_OK;
+}
+
+int32_t honu_exclusive_scan(honu_ctx *ctx, const uint64_t *d_in, uint64_t n, uint64_t *d_out,
+                            void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n > ctx->max_n) return HONU_E_WORKSPACE;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_scan(d_in, n, 1, d_out, d_out + n, ctx->partials, (hipStream_t)stream));
+    return HONU_OK;
+}
+
+int32_t honu_encode(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var, uint64_t var_len,
+                    const honu_acl *d_acl, uint64_t acl_len, const uint32_t *d_regions,
+                    uint64_t regions_len, const uint8_t *d_payload, const uint64_t *d_payload_off,
+                    uint64_t n, uint8_t *d_out, uint64_t out_cap, const uint64_t *d_out_off,
+                    int32_t *d_status, void *stream) {
+    (void)var_len;
+    (void)acl_len;
+    (void)regions_len;
+    if (!ctx) return arg_fail("ctx");
+    if (n && (!d_meta || !d_payload_off || !d_out || !d_out_off || !d_status))
+        return arg_fail("null pointer");
+    if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(launch_encode_meta(ctx->geom, d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
+                              out_cap, d_out_off, d_status, s));
+    HIPCHK(launch_encode_copy(ctx->geom, d_payload, d_payload_off, n, d_out, d_out_off, d_status, s));
+    return HONU_OK;
+}
+
+int32_t honu_marshal_batch(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
+                           uint64_t var_len, const honu_acl *d_acl, uint64_t acl_len,
+                           const uint32_t *d_regions, uint64_t regions_len,
+                           const uint8_t *d_payload, const uint64_t *d_payload_off, uint64_t n,
+                           uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off,
+                           int32_t *d_status, void *stream) {
+    int32_t st = honu_encode_sizes(ctx, d_meta, var_len, d_acl, acl_len, d_regions, regions_len,
+                                   d_payload_off, n, d_out_off, d_status, stream);
+    if (st) return st;
+    st = honu_exclusive_scan(ctx, d_out_off, n, d_out_off, stream);
+    if (st) return st;
+    return honu_encode(ctx, d_meta, d_var, var_len, d_acl, acl_len, d_regions, regions_len,
+                       d_payload, d_payload_off, n, d_out, out_cap, d_out_off, d_status, stream);
+}
+
+// ---------------------------------------------------------------------------
+// decode
+// ---------------------------------------------------------------------------
+int32_t honu_decode_parse(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                          uint64_t n, honu_meta *d_meta, honu_record_info *d_info, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n > ctx->max_n) return HONU_E_WORKSPACE;
+    if (n && (!d_rec || !d_rec_off || !d_meta || !d_info)) return arg_fail("null pointer");
+    if (!aligned(d_rec, 16) || !aligned(d_meta, 16) || !aligned(d_info, 8))
+        return arg_fail("records arena and rows must be 16-byte aligned");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_decode_parse(ctx->geom, d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
+                               ctx->counts, (hipStream_t)stream));
+    return HONU_OK;
+}
+
+int32_t honu_decode_fill(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                         uint64_t n, honu_meta *d_meta, honu_record_info *d_info,
+                         honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
+                         uint64_t regions_cap, uint8_t *d_data, uint64_t data_cap,
+                         uint64_t *d_totals, void *stream) {
+    (void)d_rec_off;
+    if (!ctx) return arg_fail("ctx");
+    if (n > ctx->max_n) return HONU_E_WORKSPACE;
+    if (!aligned(d_acl, 4) || !aligned(d_regions, 4) || !aligned(d_data, 16))
+        return arg_fail("tables 4-byte / data arena 16-byte aligned");
+    if (acl_cap && !d_acl) return arg_fail("acl table");
+    if (regions_cap && !d_regions) return arg_fail("region table");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    uint64_t *tot = d_totals ? d_totals : ctx->totals;
+    HIPCHK(launch_scan(ctx->counts, n, 3, ctx->offs, tot, ctx->partials, s));
+    HIPCHK(launch_decode_fill(ctx->geom, d_rec, n, d_meta, d_info, ctx->scratch, ctx->counts,
+                              ctx->offs, tot, d_acl, acl_cap, d_regions, regions_cap, d_data,
+                              data_cap, s));
+    if (d_data)
+        HIPCHK(launch_decode_copy(ctx->geom, d_rec, n, d_info, ctx->scratch, ctx->offs, tot, d_data, s));
+    return HONU_OK;
+}
+
+int32_t honu_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                          uint64_t n, honu_meta *d_meta, honu_record_info *d_info,
+                          honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
+                          uint64_t regions_cap, uint8_t *d_data, uint64_t data_cap,
+                          uint64_t *d_totals, void *stream) {
+    int32_t st = honu_decode_parse(ctx, d_rec, d_rec_off, n, d_meta, d_info, stream);
+    if (st) return st;
+    return honu_decode_fill(ctx, d_rec, d_rec_off, n, d_meta, d_info, d_acl, acl_cap, d_regions,
+                            regions_cap, d_data, data_cap, d_totals, stream);
+}
+
+int32_t honu_decode_keys(honu_ctx *ctx, const honu_meta *d_meta, const honu_record_info *d_info,
+                         uint64_t n, uint8_t *d_keys, int32_t *d_key_status, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_decode_keys(ctx->geom, d_meta, d_info, n, d_keys, d_key_status,
+                              (hipStream_t)stream));
+    return HONU_OK;
+}
+
+// ---------------------------------------------------------------------------
+// synthetic payload, digests, memory helpers
+// ---------------------------------------------------------------------------
+int32_t honu_gen_payload(honu_ctx *ctx, uint64_t seed, uint64_t first, uint64_t n,
+                         const uint64_t *d_payload_off, uint8_t *d_payload, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_gen_payload(ctx->geom, seed, first, n, d_payload_off, d_payload,
+                              (hipStream_t)stream));
+    return HONU_OK;
+}
+
+int32_t honu_digest_records(honu_ctx *ctx, const uint8_t *d_arena, const uint64_t *d_off,
+                            const uint64_t *d_len, uint64_t n, uint64_t *d_digest, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_digest(ctx->geom, d_arena, d_off, d_len, n, d_digest, (hipStream_t)stream));
+    return HONU_OK;
+}
+
+void *honu_host_alloc(uint64_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+void honu_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+void *honu_device_alloc(uint64_t bytes) {
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    return p;
+}
+void honu_device_free(void *p) {
+    if (p) (void)hipFree(p);
+}
+int32_t honu_memcpy_h2d(void *d_dst, const void *h_src, uint64_t bytes, void *stream) {
+    HIPCHK(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+    return HONU_OK;
+}
+int32_t honu_memcpy_d2h(void *h_dst, const void *d_src, uint64_t bytes, void *stream) {
+    HIPCHK(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    return HONU_OK;
+}
+int32_t honu_stream_sync(void *stream) {
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    return HONU_OK;
+}
+
+}  // extern "C"

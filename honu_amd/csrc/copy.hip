@@ -1,0 +1,122 @@
+// copy.hip — the HBM-bound half of the codec: moving payload bytes.
+//
+// Encode copies each record's `data` (object.go:35, lani Encode's copy,
+// encode.go:74) behind its header; materialising decode copies each
+// Data() subslice (object.go:97) into a packed, 16-byte aligned arena.
+//
+// Work is split by BYTES, not by records: the segments lie back to back in a
+// "logical" byte space (the source arena for encode, the destination arena
+// for decode), and wave w of W owns the logical range [w*B/W, (w+1)*B/W)
+// rounded to 16 bytes. A wave binary-searches its first segment once, then
+// streams forward across segment boundaries, so every wave moves the same
+// number of bytes whatever the record-size mix (XLarge records no longer
+// make stragglers) and there is no tail of half-idle CUs at the end of a
+// launch. Within a range the copy is 16 bytes per lane, UNROLL chunks in
+// flight per lane, realigned with v_alignbyte when source and destination
+// phases differ (encode: always, the header length varies).
+#include "kernels.h"
+
+namespace honu {
+
+#ifndef HONU_COPY_UNROLL
+#define HONU_COPY_UNROLL 4
+#endif
+#ifndef HONU_COPY_NT
+#define HONU_COPY_NT 0
+#endif
+
+// Segment i of an encode: src = payload[payload_off[i] ...], logical start =
+// payload_off[i], dst = out + out_off[i] + 1 + uvarint_len(len).
+struct EncodeSegments {
+    const uint8_t *payload;
+    const uint64_t *payload_off;
+    uint8_t *out;
+    const uint64_t *out_off;
+    const int32_t *status;
+
+    HONU_DEV uint64_t start(uint64_t i) const { return payload_off[i]; }
+    HONU_DEV uint64_t lo() const { return payload_off[0]; }
+    HONU_DEV bool get(uint64_t i, uint64_t &len, const uint8_t *&src, uint8_t *&dst) const {
+        if (status[i] != HONU_OK) return false;
+        const uint64_t s = payload_off[i];
+        len = payload_off[i + 1] - s;
+        src = payload + s;
+        dst = out + out_off[i] + 1 + uvarint_len(len);
+        return len != 0;
+    }
+};
+
+// Segment i of a materialising decode: logical start = offs[3i+2] (the
+// destination offset), src = rec + scratch[i].data_src.
+struct DecodeSegments {
+    const uint8_t *rec;
+    const honu_record_info *info;
+    const DecodeScratch *scratch;
+    const uint64_t *offs;
+    uint8_t *data;
+
+    HONU_DEV uint64_t start(uint64_t i) const { return offs[3 * i + 2]; }
+    HONU_DEV uint64_t lo() const { return 0; }
+    HONU_DEV bool get(uint64_t i, uint64_t &len, const uint8_t *&src, uint8_t *&dst) const {
+        if (info[i].data_status != HONU_OK) return false;
+        len = info[i].data_len;
+        src = rec + scratch[i].data_src;
+        dst = data + offs[3 * i + 2];
+        return len != 0;
+    }
+};
+
+template <class Seg>
+__global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t n,
+                                                               const uint64_t *__restrict__ total_p) {
+    const uint64_t W = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
+    const uint64_t w = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + wave_in_block();
+    const uint64_t base = seg.lo();
+    const uint64_t total = *total_p - base;
+    const uint64_t lo = base + ((total * w / W) & ~15ull);
+    const uint64_t hi = (w + 1 == W) ? base + total : base + ((total * (w + 1) / W) & ~15ull);
+    if (lo >= hi) return;
+    // largest i with start(i) <= lo
+    uint64_t a = 0, b = n;  // invariant: start(a) <= lo, answer in [a, b)
+    while (b - a > 1) {
+        const uint64_t mid = (a + b) >> 1;
+        if (seg.start(mid) <= lo) a = mid;
+        else b = mid;
+    }
+    for (uint64_t i = a; i < n; i++) {
+        const uint64_t s = seg.start(i);
+        if (s >= hi) break;
+        uint64_t len;
+        const uint8_t *src;
+        uint8_t *dst;
+        if (!seg.get(i, len, src, dst)) continue;
+        const uint64_t x = s > lo ? s : lo;
+        const uint64_t e = s + len;
+        const uint64_t y = e < hi ? e : hi;
+        if (x < y)
+            wave_copy<HONU_COPY_UNROLL, (bool)HONU_COPY_NT>(dst + (x - s), src + (x - s), y - x);
+    }
+}
+
+hipError_t launch_encode_copy(const LaunchGeom &g, const uint8_t *payload,
+                              const uint64_t *payload_off, uint64_t n, uint8_t *out,
+                              const uint64_t *out_off, const int32_t *status, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    EncodeSegments seg{payload, payload_off, out, out_off, status};
+    hipLaunchKernelGGL(k_copy_segments<EncodeSegments>, dim3(g.copy_blocks), dim3(HONU_BLOCK), 0,
+                       s, seg, n, payload_off + n);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t n,
+                              const honu_record_info *info, const DecodeScratch *scratch,
+                              const uint64_t *offs, const uint64_t *totals, uint8_t *data,
+                              hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    DecodeSegments seg{rec, info, scratch, offs, data};
+    hipLaunchKernelGGL(k_copy_segments<DecodeSegments>, dim3(g.copy_blocks), dim3(HONU_BLOCK), 0,
+                       s, seg, n, totals + 2);
+    return hipGetLastError();
+}
+
+}  // namespace honu

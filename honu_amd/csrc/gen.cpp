@@ -1,0 +1,331 @@
+// gen.cpp — deterministic synthetic workload (host side).
+//
+// Mirrors the reference benchmark generator generateRandomObject and its
+// helpers (pkg/store/object/object_test.go:195-386): the same fields, nil
+// probabilities, list lengths, value ranges and payload-size classes, with a
+// seeded counter-based PRNG per record (the reference uses unseeded
+// math/rand + crypto/rand) so that host and device, and every rank of a
+// multi-GPU run, see identical records for (seed, index).
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+using honu::splitmix64;
+
+// region.List() (pkg/region/values.go regionNames, UNKNOWN excluded)
+const uint32_t kRegions[] = {
+    1,       2,       3,       4,       1036020, 1124010, 1276090, 1356000, 1392100, 1702080,
+    1826070, 1840030, 1840040, 1840050, 1840060, 2036090, 2036091, 2036092, 2036100, 2036101,
+    2036102, 2056141, 2056142, 2056143, 2076260, 2076261, 2076262, 2124240, 2124241, 2124242,
+    2124250, 2124251, 2124252, 2152270, 2152271, 2152272, 2158001, 2158002, 2158003, 2246120,
+    2246121, 2246122, 2250210, 2250211, 2250212, 2276170, 2276171, 2276172, 2344010, 2344011,
+    2344012, 2356051, 2356052, 2356053, 2356061, 2356062, 2356063, 2360080, 2360081, 2360082,
+    2364220, 2364221, 2364222, 2376230, 2376231, 2376232, 2380150, 2380151, 2380152, 2380200,
+    2380201, 2380202, 2392020, 2392021, 2392022, 2392030, 2392031, 2392032, 2410040, 2410041,
+    2410042, 2528180, 2528181, 2528182, 2616110, 2616111, 2616112, 2702070, 2702071, 2702072,
+    2724130, 2724131, 2724132, 2756190, 2756191, 2756192, 2826160, 2826161, 2826162, 2840280,
+    2840281, 2840282, 2840285, 2840291, 2840292, 2840293, 2840300, 2840301, 2840302, 2840310,
+    2840311, 2840312, 2840320, 2840321, 2840322, 2840330, 2840331, 2840332, 2840340, 2840341,
+    2840342, 2840350, 2840351, 2840352, 2840360, 2840361, 2840362};
+const uint32_t kNumRegions = sizeof(kRegions) / sizeof(kRegions[0]);
+
+// Fixed "now" for reproducibility: 2025-01-01T00:00:00Z in UnixNano.
+const int64_t kNow = 1735689600000000000ll;
+
+// Shared constant strings at the start of every generated var arena.
+const char kSchemaName[] = "RandomSchema";          // object_test.go:244
+const char kMime[] = "application/random";          // :199
+const char kUserAgent[] = "Random User Agent v1";    // :300
+const uint64_t kOffSchema = 0, kLenSchema = 12;
+const uint64_t kOffMime = 12, kLenMime = 18;
+const uint64_t kOffUA = 30, kLenUA = 20;
+const uint64_t kVarHeader = 50;
+
+struct Rng {
+    uint64_t s;
+    uint64_t next() {
+        s += 0x9E3779B97F4A7C15ull;
+        return splitmix64(s);
+    }
+    uint32_t u32() { return (uint32_t)(next() >> 32); }
+    uint64_t intn(uint64_t n) { return next() % n; }
+    float f32() { return (float)(next() >> 40) * (1.0f / 16777216.0f); }  // [0,1)
+    uint8_t u8() { return (uint8_t)intn(255); }  // randUint8: Int31n(255), :353-355
+};
+
+struct Sink {  // null pointers: counting only
+    honu_meta *m;
+    uint8_t *var;
+    honu_acl *acl;
+    uint32_t *reg;
+    uint64_t var_n, acl_n, reg_n, pay_n;
+};
+
+void put_var(Sink &s, honu_span &sp, const uint8_t *src, uint64_t len) {
+    sp.off = s.var_n;
+    sp.len = len;
+    if (s.var) memcpy(s.var + s.var_n, src, len);
+    s.var_n += len;
+}
+
+void ulid(Rng &r, uint8_t out[16]) {  // ulid.MustNew(ulid.Now(), rand.Reader)
+    const uint64_t ms = (uint64_t)(kNow / 1000000) + r.intn(1000);
+    for (int i = 0; i < 6; i++) out[i] = (uint8_t)(ms >> (40 - 8 * i));
+    const uint64_t a = r.next(), b = r.next();
+    for (int i = 0; i < 8; i++) out[6 + i] = (uint8_t)(a >> (8 * i));
+    for (int i = 0; i < 2; i++) out[14 + i] = (uint8_t)(b >> (8 * i));
+}
+
+int64_t rand_time(Rng &r) {  // randTime :357-363
+    int64_t td = (int64_t)r.intn(31540000000000000ull);
+    if (r.f32() < 0.5f) td = -td;
+    return kNow + td;
+}
+
+uint64_t payload_len(Rng &r, int shape) {  // nRandomBytes :373-386
+    if (shape == HONU_SHAPE_MIXED) {
+        const float u = r.f32();
+        shape = u < 0.50f ? HONU_SHAPE_SMALL
+                : u < 0.80f ? HONU_SHAPE_MEDIUM
+                : u < 0.99f ? HONU_SHAPE_LARGE
+                            : HONU_SHAPE_XLARGE;
+    }
+    switch (shape) {
+    case HONU_SHAPE_SMALL: return r.intn(4096) + 512;
+    case HONU_SHAPE_MEDIUM: return r.intn(32768) + 8192;
+    case HONU_SHAPE_LARGE: return r.intn(262144) + 65536;
+    default: return r.intn(4194304) + 1048576;
+    }
+}
+
+const char kB64[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+
+// One record: generateRandomObject (:195-219). Writes the row when s.m.
+void gen_one(uint64_t seed, int shape, uint64_t index, Sink &s, honu_meta *row) {
+    Rng r{splitmix64(seed ^ splitmix64(index + 0x632BE59BD9B4E019ull))};
+    honu_meta m;
+    memset(&m, 0, sizeof m);
+    m.present = HONU_HAS_META | HONU_HAS_VERSION;
+    // randVersion :221-235
+    m.pid = r.u32();
+    m.vid = r.next();
+    m.region = kRegions[r.intn(kNumRegions)];
+    m.tombstone = r.f32() < 0.25f;
+    m.version_created = rand_time(r);
+    if (r.f32() < 0.9f) {
+        m.present |= HONU_HAS_PARENT;
+        m.parent_pid = r.u32();
+        m.parent_vid = r.next();
+    }
+    // randSchema :237-251
+    if (!(r.f32() < 0.1f)) {
+        m.present |= HONU_HAS_SCHEMA;
+        m.schema_name = honu_span{kOffSchema, kLenSchema};
+        m.schema_major = r.u32();
+        m.schema_minor = r.u32();
+        m.schema_patch = r.u32();
+    }
+    m.mime = honu_span{kOffMime, kLenMime};
+    ulid(r, m.owner);
+    ulid(r, m.group);
+    m.permissions = r.u8();
+    // randACL :253-268
+    if (!(r.f32() < 0.1f)) {
+        const uint64_t na = r.intn(64) + 1;
+        m.acl_off = s.acl_n;
+        m.acl_count = na;
+        for (uint64_t i = 0; i < na; i++) {
+            honu_acl a;
+            memset(&a, 0, sizeof a);
+            ulid(r, a.client_id);
+            a.permissions = r.u8();
+            a.present = 1;
+            if (s.acl) s.acl[s.acl_n] = a;
+            s.acl_n++;
+        }
+    }
+    // randRegions :272-284
+    if (!(r.f32() < 0.1f)) {
+        const uint64_t nr = r.intn(9) + 1;
+        m.regions_off = s.reg_n;
+        m.regions_count = nr;
+        for (uint64_t i = 0; i < nr; i++) {
+            const uint32_t v = kRegions[r.intn(kNumRegions)];
+            if (s.reg) s.reg[s.reg_n] = v;
+            s.reg_n++;
+        }
+    }
+    // randPublisher :290-302 (net.IPv4 -> 16-byte form)
+    if (!(r.f32() < 0.1f)) {
+        m.present |= HONU_HAS_PUBLISHER;
+        ulid(r, m.publisher_id);
+        ulid(r, m.client_id);
+        uint8_t ip[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0xff, 0xff, 0, 0, 0, 0};
+        for (int i = 0; i < 4; i++) ip[12 + i] = r.u8();
+        put_var(s, m.ip_address, ip, 16);
+        m.user_agent = honu_span{kOffUA, kLenUA};
+    }
+    // randEncryption :304-330
+    if (!(r.f32() < 0.1f)) {
+        m.present |= HONU_HAS_ENCRYPTION;
+        static const uint8_t algs[4] = {0 /*Plaintext*/, 3 /*AES128_GCM*/, 2 /*AES192_GCM*/,
+                                        1 /*AES256_GCM*/};
+        m.encryption_alg = algs[r.intn(4)];
+        if (m.encryption_alg != 0) {
+            m.sealing_alg = 5;    // RSA_OEAP_SHA512
+            m.signature_alg = 4;  // HMAC_SHA256
+            uint8_t raw[16], txt[22];
+            for (int i = 0; i < 16; i++) raw[i] = (uint8_t)r.next();
+            // base64.RawStdEncoding of 16 bytes -> 22 chars
+            uint32_t bi = 0;
+            for (int i = 0; i < 15; i += 3) {
+                const uint32_t v = (raw[i] << 16) | (raw[i + 1] << 8) | raw[i + 2];
+                txt[bi++] = kB64[(v >> 18) & 63];
+                txt[bi++] = kB64[(v >> 12) & 63];
+                txt[bi++] = kB64[(v >> 6) & 63];
+                txt[bi++] = kB64[v & 63];
+            }
+            txt[bi++] = kB64[raw[15] >> 2];
+            txt[bi++] = kB64[(raw[15] & 3) << 4];
+            put_var(s, m.public_key_id, txt, 22);
+            uint8_t buf[256];
+            for (int i = 0; i < 32; i++) buf[i] = (uint8_t)r.next();
+            put_var(s, m.encryption_key, buf, 32);
+            for (int i = 0; i < 32; i++) buf[i] = (uint8_t)r.next();
+            put_var(s, m.hmac_secret, buf, 32);
+            for (int i = 0; i < 256; i += 8) {
+                const uint64_t v = r.next();
+                memcpy(buf + i, &v, 8);
+            }
+            put_var(s, m.signature, buf, 256);
+        }
+    }
+    // randCompression :332-351
+    if (!(r.f32() < 0.1f)) {
+        m.present |= HONU_HAS_COMPRESSION;
+        m.compression_alg = (uint8_t)r.intn(5);
+        if (m.compression_alg == 1 || m.compression_alg == 2) m.compression_level = (int64_t)r.intn(9) + 1;
+    }
+    m.flags = r.u8();
+    m.created = rand_time(r);
+    m.modified = rand_time(r);
+    s.pay_n += payload_len(r, shape);
+    if (row) *row = m;
+}
+
+struct Part {
+    uint64_t first, n;
+    uint64_t var0, acl0, reg0, pay0;  // bases
+    uint64_t var_n, acl_n, reg_n, pay_n;  // totals of this part
+};
+
+int num_threads(uint64_t n) {
+    unsigned hc = std::thread::hardware_concurrency();
+    if (hc == 0) hc = 1;
+    if (hc > 16) hc = 16;
+    uint64_t t = n / 4096 + 1;
+    return (int)std::min<uint64_t>(hc, t);
+}
+
+template <class F> void parallel(int nt, F f) {
+    if (nt <= 1) {
+        f(0);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++) th.emplace_back(f, t);
+    for (auto &x : th) x.join();
+}
+
+std::vector<Part> plan(uint64_t seed, int shape, uint64_t first, uint64_t n) {
+    const int nt = num_threads(n);
+    std::vector<Part> parts(nt);
+    for (int t = 0; t < nt; t++) {
+        parts[t].first = first + n * t / nt;
+        parts[t].n = first + n * (t + 1) / nt - parts[t].first;
+    }
+    parallel(nt, [&](int t) {
+        Sink s{nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0};
+        for (uint64_t i = 0; i < parts[t].n; i++) gen_one(seed, shape, parts[t].first + i, s, nullptr);
+        parts[t].var_n = s.var_n;
+        parts[t].acl_n = s.acl_n;
+        parts[t].reg_n = s.reg_n;
+        parts[t].pay_n = s.pay_n;
+    });
+    uint64_t v = kVarHeader, a = 0, r = 0, p = 0;
+    for (auto &pt : parts) {
+        pt.var0 = v;
+        pt.acl0 = a;
+        pt.reg0 = r;
+        pt.pay0 = p;
+        v += pt.var_n;
+        a += pt.acl_n;
+        r += pt.reg_n;
+        p += pt.pay_n;
+    }
+    return parts;
+}
+
+}  // namespace
+
+extern "C" {
+
+void honu_gen_totals(uint64_t seed, int32_t shape, uint64_t first, uint64_t n, uint64_t totals[4]) {
+    std::vector<Part> parts = plan(seed, shape, first, n);
+    totals[0] = kVarHeader;
+    totals[1] = totals[2] = totals[3] = 0;
+    for (auto &p : parts) {
+        totals[0] += p.var_n;
+        totals[1] += p.acl_n;
+        totals[2] += p.reg_n;
+        totals[3] += p.pay_n;
+    }
+}
+
+void honu_gen_meta(uint64_t seed, int32_t shape, uint64_t first, uint64_t n, honu_meta *meta,
+                   uint8_t *var_arena, honu_acl *acl, uint32_t *regions, uint64_t *payload_off) {
+    memcpy(var_arena + kOffSchema, kSchemaName, kLenSchema);
+    memcpy(var_arena + kOffMime, kMime, kLenMime);
+    memcpy(var_arena + kOffUA, kUserAgent, kLenUA);
+    std::vector<Part> parts = plan(seed, shape, first, n);
+    parallel((int)parts.size(), [&](int t) {
+        const Part &pt = parts[t];
+        Sink s{nullptr, var_arena, acl, regions, pt.var0, pt.acl0, pt.reg0, pt.pay0};
+        for (uint64_t i = 0; i < pt.n; i++) {
+            const uint64_t li = pt.first - first + i;
+            payload_off[li] = s.pay_n;
+            gen_one(seed, shape, pt.first + i, s, &meta[li]);
+        }
+    });
+    uint64_t tot = 0;
+    for (auto &p : parts) tot += p.pay_n;
+    payload_off[n] = tot;
+}
+
+void honu_gen_payload_host(uint64_t seed, uint64_t first, uint64_t n, const uint64_t *payload_off,
+                           uint8_t *payload) {
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t s = payload_off[i], len = payload_off[i + 1] - s;
+        for (uint64_t k = 0; k < len; k++)
+            payload[s + k] = (uint8_t)(honu::payload_word(seed, first + i, k >> 3) >> (8 * (k & 7)));
+    }
+}
+
+uint64_t honu_digest_host(const uint8_t *p, uint64_t len) {
+    uint64_t acc = honu::splitmix64(len);
+    for (uint64_t k = 0; 8 * k < len; k++) {
+        uint64_t w = 0;
+        for (uint64_t j = 0; j < 8 && 8 * k + j < len; j++) w |= (uint64_t)p[8 * k + j] << (8 * j);
+        acc += honu::digest_term(w, k);
+    }
+    return acc;
+}
+
+}  // extern "C"

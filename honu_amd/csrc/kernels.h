@@ -1,0 +1,71 @@
+// kernels.h — launch wrappers shared between the kernel translation units and
+// the C ABI (api.hip). Every wrapper is asynchronous on `stream` and returns a
+// hipError_t from the launch.
+#pragma once
+
+#include "common.h"
+
+// LDS budget per wave for the Metadata tail writer (encode.hip) and the
+// decode window (decode.hip). Generated tails are 0.15-1.8 KB; longer tails
+// take the in-place fallback (encode) or re-stage the window (decode).
+#define ENC_TAIL_LDS 4096
+#define DEC_WIN 2048
+
+namespace honu {
+
+// Per-record scratch handed from honu_decode_parse to honu_decode_fill.
+struct DecodeScratch {
+    uint64_t acl_pos;     // absolute offset of the first ACL entry flag
+    uint64_t regions_pos; // absolute offset of the first region varint
+    uint64_t data_src;    // absolute offset of the payload (Data() subslice)
+    uint64_t rec_end;     // absolute end of the record
+};
+
+struct LaunchGeom {
+    int num_cu;
+    int per_record_blocks;  // cap on blocks for one-wave-per-record kernels
+    int copy_blocks;        // blocks of the byte-balanced copy kernel
+};
+
+hipError_t launch_encode_sizes(const LaunchGeom &g, const honu_meta *meta, uint64_t var_len,
+                               const honu_acl *acl, uint64_t acl_len, const uint32_t *reg,
+                               uint64_t reg_len, const uint64_t *payload_off, uint64_t n,
+                               uint64_t *sizes, int32_t *status, hipStream_t s);
+hipError_t launch_encode_meta(const LaunchGeom &g, const honu_meta *meta, const uint8_t *var,
+                              const honu_acl *acl, const uint32_t *reg,
+                              const uint64_t *payload_off, uint64_t n, uint8_t *out,
+                              uint64_t out_cap, const uint64_t *out_off, int32_t *status,
+                              hipStream_t s);
+hipError_t launch_encode_copy(const LaunchGeom &g, const uint8_t *payload,
+                              const uint64_t *payload_off, uint64_t n, uint8_t *out,
+                              const uint64_t *out_off, const int32_t *status, hipStream_t s);
+
+hipError_t launch_decode_parse(const LaunchGeom &g, const uint8_t *rec, const uint64_t *rec_off,
+                               uint64_t n, honu_meta *meta, honu_record_info *info,
+                               DecodeScratch *scratch, uint64_t *counts, hipStream_t s);
+hipError_t launch_decode_fill(const LaunchGeom &g, const uint8_t *rec, uint64_t n,
+                              honu_meta *meta, honu_record_info *info,
+                              const DecodeScratch *scratch, const uint64_t *counts,
+                              const uint64_t *offs, const uint64_t *totals, honu_acl *acl,
+                              uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap, uint8_t *data,
+                              uint64_t data_cap, hipStream_t s);
+hipError_t launch_decode_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t n,
+                              const honu_record_info *info, const DecodeScratch *scratch,
+                              const uint64_t *offs, const uint64_t *totals, uint8_t *data,
+                              hipStream_t s);
+hipError_t launch_decode_keys(const LaunchGeom &g, const honu_meta *meta,
+                              const honu_record_info *info, uint64_t n, uint8_t *keys,
+                              int32_t *key_status, hipStream_t s);
+
+// Exclusive scan of K interleaved u64 columns: out[i*K+c] = sum_{j<i} in[j*K+c];
+// totals[c] = full sum. `partials` needs scan_partials_len(n, K) u64.
+uint64_t scan_partials_len(uint64_t n, int K);
+hipError_t launch_scan(const uint64_t *in, uint64_t n, int K, uint64_t *out, uint64_t *totals,
+                       uint64_t *partials, hipStream_t s);
+
+hipError_t launch_gen_payload(const LaunchGeom &g, uint64_t seed, uint64_t first, uint64_t n,
+                              const uint64_t *payload_off, uint8_t *payload, hipStream_t s);
+hipError_t launch_digest(const LaunchGeom &g, const uint8_t *arena, const uint64_t *off,
+                         const uint64_t *len, uint64_t n, uint64_t *digest, hipStream_t s);
+
+}  // namespace honu

@@ -1,0 +1,337 @@
+/*
+ * honu_codec.h — C ABI of the MI355X-native batch object-record codec.
+ *
+ * This is the drop-in boundary for Honu's reflection-free object codec
+ * (rotationalio/honu, pkg/store/object + pkg/store/lani + pkg/store/metadata).
+ * The reference has no FFI at all (it is pure Go, CGO_ENABLED=0); the entry
+ * points below are what a cgo shim behind a `honu_hip` build tag binds so that
+ * pkg/store keeps its Go API (see INTEGRATION.md for the cgo stub).
+ *
+ *   reference (Go, one record per call)               this ABI (one batch per call)
+ *   -----------------------------------------------   ------------------------------------------
+ *   object.Marshal(meta, data)  object.go:24-45        honu_encode_sizes + honu_exclusive_scan
+ *                                                       + honu_encode   (or honu_marshal_batch)
+ *   Object.Metadata()           object.go:66-83        honu_decode_parse + honu_decode_fill
+ *   Object.Data()               object.go:85-99          (or honu_decode_batch); per-record
+ *   Object.Tombstone()          object.go:103-112        results land in honu_record_info
+ *   Object.StorageVersion()     object.go:47-52
+ *   Object.Key()                object.go:57-64        honu_decode_keys (29-byte keys.Key column)
+ *   lani.Encodable.Size()       lani/lani.go:9-12      (host only; Size() is a Grow hint, not bytes)
+ *
+ * Conventions
+ *   - Every pointer argument named d_* is DEVICE memory (hipMalloc / torch
+ *     tensor storage) unless stated; every call is asynchronous on `stream`
+ *     (a hipStream_t passed as void*, NULL = the null stream). No call
+ *     allocates, frees or synchronises, so a sequence of calls can be
+ *     captured into a hipGraph.
+ *   - Batches are CSR: record i occupies bytes [off[i], off[i+1]) of an arena.
+ *   - Functions return an honu_status for argument errors (HONU_E_ARG,
+ *     HONU_E_WORKSPACE, HONU_E_HIP); per-record outcomes are written to device
+ *     status arrays using the same enum.
+ *   - The library is gfx950-only; it fails loudly (HONU_E_NO_DEVICE) when no
+ *     gfx950 device is present. There is no CPU fallback.
+ */
+#ifndef HONU_CODEC_H
+#define HONU_CODEC_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HONU_ABI_VERSION 1u
+#define HONU_STORAGE_VERSION 1u /* object.StorageVersion, object.go:14 */
+#define HONU_ULID_LEN 16
+#define HONU_KEY_LEN 29         /* keys.keySize, keys/keys.go:14 */
+
+/* ------------------------------------------------------------------------ */
+/* Status codes. Per-record codes map 1:1 to the Go sentinels.              */
+/* ------------------------------------------------------------------------ */
+typedef enum honu_status {
+    HONU_OK = 0,
+    HONU_ERR_BAD_VERSION = 1,    /* object.ErrBadVersion     object/errors.go:6 */
+    HONU_ERR_MALFORMED = 2,      /* object.ErrMalformed      object/errors.go:7 */
+    HONU_ERR_EOF = 3,            /* io.EOF                   lani/decode.go:95,129,151,173,195,211 */
+    HONU_ERR_UNEXPECTED_EOF = 4, /* io.ErrUnexpectedEOF      lani/decode.go:47,200,215 */
+    HONU_ERR_NO_LENGTH = 5,      /* lani.ErrNoLength         lani/errors.go:8 */
+    HONU_ERR_PARSE_BOOLEAN = 6,  /* lani.ErrParseBoolean     lani/errors.go:9 */
+    HONU_ERR_PARSE_VARINT = 7,   /* lani.ErrParseVarInt      lani/errors.go:10 */
+    HONU_ERR_PANIC = 8,          /* input on which the Go reference panics (slice
+                                    out of range object.go:77,97; makeslice
+                                    decode.go:50, metadata.go:255, region.go:160;
+                                    nil *Metadata in Marshal metadata.go:66) */
+    HONU_ERR_CAPACITY = 9,       /* an output arena/table was too small (ABI only) */
+    HONU_ERR_INPUT = 10,         /* an encode input span/list points outside its arena (ABI only) */
+    /* call-level errors (returned, never written per record) */
+    HONU_E_ARG = -1,
+    HONU_E_WORKSPACE = -2,       /* n exceeds the context's reserved record count */
+    HONU_E_HIP = -3,             /* a HIP runtime call failed */
+    HONU_E_NO_DEVICE = -4        /* no gfx950 device / kernels not loadable */
+} honu_status;
+
+/* ------------------------------------------------------------------------ */
+/* Data layout                                                               */
+/* ------------------------------------------------------------------------ */
+
+/* A byte range inside an arena. Zero length == nil == empty: lani frames of
+ * length 0 decode to nil (lani/decode.go:37-39) and nil/empty encode alike. */
+typedef struct honu_span {
+    uint64_t off;
+    uint64_t len;
+} honu_span;
+
+/* Presence bits of honu_meta.present (the lani nil-flag bytes). */
+enum {
+    HONU_HAS_META = 1u << 0,        /* object-level Metadata nil flag (object.go:40) */
+    HONU_HAS_VERSION = 1u << 1,     /* Metadata.Version      metadata.go:20 */
+    HONU_HAS_PARENT = 1u << 2,      /* Version.Parent        version.go:17 */
+    HONU_HAS_SCHEMA = 1u << 3,      /* Metadata.Schema       metadata.go:21 */
+    HONU_HAS_PUBLISHER = 1u << 4,   /* Metadata.Publisher    metadata.go:28 */
+    HONU_HAS_ENCRYPTION = 1u << 5,  /* Metadata.Encryption   metadata.go:29 */
+    HONU_HAS_COMPRESSION = 1u << 6, /* Metadata.Compression  metadata.go:30 */
+    HONU_REGIONS_NONNIL = 1u << 7   /* set by decode: Regions.Decode always makes a
+                                       (possibly empty) slice, region.go:160 */
+};
+
+/* One metadata.Metadata (metadata.go:17-35) flattened into a fixed 352-byte
+ * row. Rows are the encode input and the decode output.
+ *   encode: spans index `var_arena`, acl_off/acl_count index the ACL table,
+ *           regions_off/regions_count index the region table.
+ *   decode: spans are ABSOLUTE offsets into the records arena (zero copy, like
+ *           lani.DecodeFixed), acl_off/regions_off index the output tables.
+ * Times are Go UnixNano with 0 <=> time.Time{}.IsZero() (lani/encode.go:201-206,
+ * decode.go:224-237). Fields of absent (nil) sub-structs are zero on decode. */
+typedef struct honu_meta {
+    uint32_t present;            /*   0 HONU_HAS_* bits */
+    uint8_t permissions;         /*   4 Metadata.Permissions */
+    uint8_t flags;               /*   5 Metadata.Flags */
+    uint8_t tombstone;           /*   6 Version.Tombstone (bool, 0/1) */
+    uint8_t compression_alg;     /*   7 Compression.Algorithm */
+    uint8_t sealing_alg;         /*   8 Encryption.SealingAlgorithm */
+    uint8_t encryption_alg;      /*   9 Encryption.EncryptionAlgorithm */
+    uint8_t signature_alg;       /*  10 Encryption.SignatureAlgorithm */
+    uint8_t _pad0;               /*  11 */
+    uint32_t region;             /*  12 Version.Region */
+    uint64_t vid;                /*  16 Version.Scalar.VID */
+    uint32_t pid;                /*  24 Version.Scalar.PID */
+    uint32_t parent_pid;         /*  28 Version.Parent.PID */
+    uint64_t parent_vid;         /*  32 Version.Parent.VID */
+    int64_t version_created;     /*  40 Version.Created */
+    uint32_t schema_major;       /*  48 SchemaVersion.Major */
+    uint32_t schema_minor;       /*  52 */
+    uint32_t schema_patch;       /*  56 */
+    uint32_t _pad1;              /*  60 */
+    int64_t compression_level;   /*  64 Compression.Level */
+    int64_t created;             /*  72 Metadata.Created */
+    int64_t modified;            /*  80 Metadata.Modified */
+    uint64_t _pad2;              /*  88 */
+    uint8_t object_id[16];       /*  96 Metadata.ObjectID */
+    uint8_t collection_id[16];   /* 112 Metadata.CollectionID */
+    uint8_t owner[16];           /* 128 Metadata.Owner */
+    uint8_t group[16];           /* 144 Metadata.Group */
+    uint8_t publisher_id[16];    /* 160 Publisher.PublisherID */
+    uint8_t client_id[16];       /* 176 Publisher.ClientID */
+    honu_span schema_name;       /* 192 SchemaVersion.Name */
+    honu_span mime;              /* 208 Metadata.MIME */
+    honu_span ip_address;        /* 224 Publisher.IPAddress (net.IP bytes) */
+    honu_span user_agent;        /* 240 Publisher.UserAgent */
+    honu_span public_key_id;     /* 256 Encryption.PublicKeyID */
+    honu_span encryption_key;    /* 272 Encryption.EncryptionKey */
+    honu_span hmac_secret;       /* 288 Encryption.HMACSecret */
+    honu_span signature;         /* 304 Encryption.Signature */
+    uint64_t acl_off;            /* 320 first entry in the ACL table */
+    uint64_t acl_count;          /* 328 len(Metadata.ACL); 0 <=> nil */
+    uint64_t regions_off;        /* 336 first entry in the region table */
+    uint64_t regions_count;      /* 344 len(Metadata.WriteRegions) */
+} honu_meta;                     /* 352 */
+
+/* One *metadata.AccessControl (acls.go:12-15); present==0 is a nil pointer
+ * in the ACL slice (encoded as a single 0x00 flag byte). */
+typedef struct honu_acl {
+    uint8_t client_id[16];
+    uint8_t permissions;
+    uint8_t present;
+    uint8_t _pad[2];
+} honu_acl; /* 20 */
+
+/* Per-record decode results: the Object methods object.go:47-112. */
+typedef struct honu_record_info {
+    uint64_t data_off;       /* payload: absolute offset in the records arena
+                                (zero copy, like Data()'s subslice) or in the
+                                data arena when materialising */
+    uint64_t data_len;       /* len(Data()); 0 also for nil */
+    int32_t data_status;     /* error of Object.Data() */
+    int32_t meta_status;     /* error of Object.Metadata() */
+    uint8_t storage_version; /* Object.StorageVersion() */
+    uint8_t tombstone;       /* Object.Tombstone() */
+    uint8_t _pad[6];
+} honu_record_info; /* 32 */
+
+/* ------------------------------------------------------------------------ */
+/* Context                                                                   */
+/* ------------------------------------------------------------------------ */
+typedef struct honu_ctx honu_ctx;
+
+/* Create a context on HIP device `device` with scratch for batches of up to
+ * `max_records` records (scan partials, decode list positions). Allocation
+ * happens here and only here. Returns NULL and sets *err on failure.
+ * The scratch is per context: calls that use it (scan, decode) issued on
+ * different streams concurrently need one context each. Arenas: the records
+ * arena, the materialised data arena and row arrays must be 16-byte aligned,
+ * ACL and region tables 4-byte aligned (hipMalloc gives 256). */
+honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err);
+void honu_ctx_destroy(honu_ctx *ctx);
+uint64_t honu_ctx_max_records(const honu_ctx *ctx);
+
+/* ABI self-description, used by bindings to check struct layouts. */
+uint32_t honu_abi_version(void);
+uint64_t honu_sizeof_meta(void);
+uint64_t honu_sizeof_acl(void);
+uint64_t honu_sizeof_record_info(void);
+const char *honu_status_string(int32_t status);
+/* Text of the last call-level failure on this thread (HIP error text etc.). */
+const char *honu_last_error(void);
+
+/* ------------------------------------------------------------------------ */
+/* Encode: object.Marshal over a batch (object.go:24-45)                     */
+/* ------------------------------------------------------------------------ */
+
+/* Exact encoded length of every record: 1 + uvarint(len data) + len data +
+ * 1 + len(Metadata encoding) (object.go:30,35,40). A record that cannot be
+ * encoded gets size 0 and d_status[i] = HONU_ERR_PANIC when HONU_HAS_META is
+ * clear (Marshal(nil, …) dereferences nil, metadata.go:66) or HONU_ERR_INPUT
+ * when a span or list lies outside its arena; otherwise d_status[i] = HONU_OK.
+ * Arguments as for honu_encode. */
+int32_t honu_encode_sizes(honu_ctx *ctx, const honu_meta *d_meta, uint64_t var_len,
+                          const honu_acl *d_acl, uint64_t acl_len, const uint32_t *d_regions,
+                          uint64_t regions_len, const uint64_t *d_payload_off, uint64_t n,
+                          uint64_t *d_sizes, int32_t *d_status, void *stream);
+
+/* Exclusive prefix sum: d_out[i] = sum(d_in[0..i)), d_out[n] = total.
+ * d_out must hold n+1 values and may alias d_in only if equal. */
+int32_t honu_exclusive_scan(honu_ctx *ctx, const uint64_t *d_in, uint64_t n, uint64_t *d_out,
+                            void *stream);
+
+/* Encode record i into d_out[d_out_off[i], d_out_off[i+1]). d_out_off comes
+ * from honu_encode_sizes + honu_exclusive_scan and d_status from
+ * honu_encode_sizes: records whose status is not HONU_OK are skipped, records
+ * whose range exceeds out_cap get HONU_ERR_CAPACITY; nothing is written for a
+ * failed record.
+ *   d_var, var_len:        byte arena indexed by honu_meta spans
+ *   d_acl, acl_len:        ACL table indexed by acl_off/acl_count
+ *   d_regions, regions_len: uint32 region table
+ *   d_payload, d_payload_off: CSR payload arena (the `data` argument) */
+int32_t honu_encode(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var, uint64_t var_len,
+                    const honu_acl *d_acl, uint64_t acl_len, const uint32_t *d_regions,
+                    uint64_t regions_len, const uint8_t *d_payload, const uint64_t *d_payload_off,
+                    uint64_t n, uint8_t *d_out, uint64_t out_cap, const uint64_t *d_out_off,
+                    int32_t *d_status, void *stream);
+
+/* sizes + scan + encode in one call; d_out_off (n+1) is produced here. */
+int32_t honu_marshal_batch(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
+                           uint64_t var_len, const honu_acl *d_acl, uint64_t acl_len,
+                           const uint32_t *d_regions, uint64_t regions_len,
+                           const uint8_t *d_payload, const uint64_t *d_payload_off, uint64_t n,
+                           uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off,
+                           int32_t *d_status, void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* Decode: Object.Metadata() + Object.Data() over a batch (object.go:66-99)  */
+/* ------------------------------------------------------------------------ */
+
+/* Phase 1: parse every record of the CSR batch (d_rec, d_rec_off[n+1]):
+ * header, payload descriptor and the full Metadata walk with the exact
+ * lani error semantics. Writes d_meta rows (list counts set, list offsets
+ * not yet) and d_info. List positions and counts are kept in the context. */
+int32_t honu_decode_parse(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                          uint64_t n, honu_meta *d_meta, honu_record_info *d_info, void *stream);
+
+/* Phase 2: assign table offsets (exclusive scans over the counts), fill
+ * the ACL and region tables, and when d_data != NULL materialise every
+ * payload into d_data at 16-byte aligned offsets (d_info[i].data_off is then
+ * relative to d_data). d_totals (device, 3 x u64) receives the totals the
+ * batch needs: ACL entries, region entries, data-arena bytes. Records whose
+ * outputs do not fit get HONU_ERR_CAPACITY in meta_status / data_status. */
+int32_t honu_decode_fill(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                         uint64_t n, honu_meta *d_meta, honu_record_info *d_info,
+                         honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
+                         uint64_t regions_cap, uint8_t *d_data, uint64_t data_cap,
+                         uint64_t *d_totals, void *stream);
+
+/* parse + fill in one call. */
+int32_t honu_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                          uint64_t n, honu_meta *d_meta, honu_record_info *d_info,
+                          honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
+                          uint64_t regions_cap, uint8_t *d_data, uint64_t data_cap,
+                          uint64_t *d_totals, void *stream);
+
+/* Object.Key() (object.go:57-64 -> keys.New, keys/keys.go:42-51) for every
+ * decoded record: 0x01 | ObjectID | BE64(VID) | BE32(PID), 29 bytes per
+ * record at d_keys + 29*i. d_key_status[i] = meta_status, or HONU_ERR_PANIC
+ * when the decoded Version is nil (metadata.go:54 dereferences it). */
+int32_t honu_decode_keys(honu_ctx *ctx, const honu_meta *d_meta, const honu_record_info *d_info,
+                         uint64_t n, uint8_t *d_keys, int32_t *d_key_status, void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* Synthetic workload (bench/test support; mirrors the reference benchmark   */
+/* generator object_test.go:195-386 with a seeded counter-based PRNG).       */
+/* ------------------------------------------------------------------------ */
+typedef enum honu_shape {
+    HONU_SHAPE_SMALL = 0,  /* payload U[512, 4608)        object_test.go:376 */
+    HONU_SHAPE_MEDIUM = 1, /* payload U[8192, 40960)      :378 */
+    HONU_SHAPE_LARGE = 2,  /* payload U[65536, 327680)    :380 */
+    HONU_SHAPE_XLARGE = 3, /* payload U[1048576, 5242880) :382 */
+    HONU_SHAPE_MIXED = 4   /* per record: S .50 / M .30 / L .19 / XL .01 */
+} honu_shape;
+
+/* Host-side sizing pass for records [first, first+n) of the synthetic batch
+ * (seed, shape): totals of var-arena bytes, ACL entries, region entries and
+ * payload bytes, so the caller can allocate before honu_gen_meta. */
+void honu_gen_totals(uint64_t seed, int32_t shape, uint64_t first, uint64_t n,
+                     uint64_t totals[4]);
+
+/* Host-side: fill HOST arrays for records [first, first+n): rows, var arena,
+ * ACL table, region table and the CSR payload offsets (n+1, starting at 0).
+ * Offsets in rows are relative to the given arrays. */
+void honu_gen_meta(uint64_t seed, int32_t shape, uint64_t first, uint64_t n, honu_meta *meta,
+                   uint8_t *var_arena, honu_acl *acl, uint32_t *regions, uint64_t *payload_off);
+
+/* Payload bytes of record `index` of the synthetic batch are
+ * honu_payload_byte(seed, index, k) for k in [0, len). Host and device
+ * produce identical bytes. */
+void honu_gen_payload_host(uint64_t seed, uint64_t first, uint64_t n, const uint64_t *payload_off,
+                           uint8_t *payload);
+int32_t honu_gen_payload(honu_ctx *ctx, uint64_t seed, uint64_t first, uint64_t n,
+                         const uint64_t *d_payload_off, uint8_t *d_payload, void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* Verification helpers (device, used by tests and bench at full size)       */
+/* ------------------------------------------------------------------------ */
+
+/* Position-aware 64-bit digest of every record's bytes: splitmix64(len) +
+ * sum over the zero-padded little-endian 8-byte words w_k of
+ * splitmix64(w_k + k * 0x9E3779B97F4A7C15). d_digest[i] covers
+ * d_arena[d_off[i], d_off[i+1]) or, when d_len != NULL,
+ * [d_off[i], d_off[i]+d_len[i]) with d_off of length n. */
+int32_t honu_digest_records(honu_ctx *ctx, const uint8_t *d_arena, const uint64_t *d_off,
+                            const uint64_t *d_len, uint64_t n, uint64_t *d_digest, void *stream);
+/* The same digest of one host byte run. */
+uint64_t honu_digest_host(const uint8_t *p, uint64_t len);
+
+/* ------------------------------------------------------------------------ */
+/* Host memory helpers (pinned buffers for the host<->device path)          */
+/* ------------------------------------------------------------------------ */
+void *honu_host_alloc(uint64_t bytes);  /* hipHostMalloc, NULL on failure */
+void honu_host_free(void *p);
+void *honu_device_alloc(uint64_t bytes); /* hipMalloc on the current device */
+void honu_device_free(void *p);
+int32_t honu_memcpy_h2d(void *d_dst, const void *h_src, uint64_t bytes, void *stream);
+int32_t honu_memcpy_d2h(void *h_dst, const void *d_src, uint64_t bytes, void *stream);
+int32_t honu_stream_sync(void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HONU_CODEC_H */

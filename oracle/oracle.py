@@ -1,0 +1,128 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes binding of the CPU oracle (libhonu_oracle.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, and only as the checker / CPU baseline; honu_amd never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhonu_oracle.so")
+_lib = None
+P, U64, I32 = C.c_void_p, C.c_uint64, C.c_int32
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        build()
+    lib = C.CDLL(LIB_PATH)
+    protos = {
+        "oracle_put_uvarint": (C.c_int, [P, U64]),
+        "oracle_uvarint": (C.c_int, [P, U64, P]),
+        "oracle_put_varint": (C.c_int, [P, C.c_int64]),
+        "oracle_varint": (C.c_int, [P, U64, P]),
+        "oracle_size_bound": (C.c_int64, [C.c_int, P]),
+        "oracle_marshal": (C.c_int, [P, P, U64, P, U64, P, U64, P, U64, P, U64, P]),
+        "oracle_decode": (None, [P, U64, U64, P, P, P, U64, P, U64, P, P]),
+        "oracle_marshal_batch": (C.c_int, [P, P, U64, P, U64, P, U64, P, P, U64, P, U64, P, P]),
+        "oracle_decode_batch": (C.c_int, [P, P, U64, P, P, P, U64, P, U64, P, U64, P]),
+        "oracle_key": (C.c_int, [P, I32, P]),
+    }
+    for name, (res, args) in protos.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _p(a):
+    return 0 if a is None else a.ctypes.data
+
+
+def put_uvarint(x: int) -> bytes:
+    buf = (C.c_uint8 * 10)()
+    k = load().oracle_put_uvarint(buf, x)
+    return bytes(buf[:k])
+
+
+def uvarint(b: bytes):
+    out = C.c_uint64(0)
+    k = load().oracle_uvarint(b, len(b), C.byref(out))
+    return out.value, k
+
+
+def put_varint(x: int) -> bytes:
+    buf = (C.c_uint8 * 10)()
+    k = load().oracle_put_varint(buf, x)
+    return bytes(buf[:k])
+
+
+def varint(b: bytes):
+    out = C.c_int64(0)
+    k = load().oracle_varint(b, len(b), C.byref(out))
+    return out.value, k
+
+
+def size_bound(which: int, row) -> int:
+    row = np.ascontiguousarray(row)
+    return load().oracle_size_bound(which, _p(row))
+
+
+def marshal_batch(hb):
+    """(records arena, out_off[n+1], status[n]) for a honu_amd.metadata.HostBatch."""
+    lib = load()
+    n = len(hb.meta)
+    out_off = np.zeros(n + 1, np.uint64)
+    status = np.zeros(n, np.int32)
+    lib.oracle_marshal_batch(_p(hb.meta), _p(hb.var), len(hb.var), _p(hb.acl), len(hb.acl),
+                             _p(hb.regions), len(hb.regions), _p(hb.payload), _p(hb.payload_off),
+                             n, None, 0, _p(out_off), _p(status))
+    total = int(out_off[n])
+    out = np.zeros(max(total, 1), np.uint8)
+    lib.oracle_marshal_batch(_p(hb.meta), _p(hb.var), len(hb.var), _p(hb.acl), len(hb.acl),
+                             _p(hb.regions), len(hb.regions), _p(hb.payload), _p(hb.payload_off),
+                             n, _p(out), total, _p(out_off), _p(status))
+    return out[:total], out_off, status
+
+
+def decode_batch(rec: np.ndarray, rec_off: np.ndarray, materialize: bool = False):
+    """(meta rows, info, acl table, region table, data arena | None, totals[3])."""
+    from honu_amd.metadata import ACL_DTYPE, INFO_DTYPE, META_DTYPE
+    lib = load()
+    n = len(rec_off) - 1
+    rec = np.ascontiguousarray(rec, np.uint8)
+    if rec.size == 0:
+        rec = np.zeros(1, np.uint8)
+    rec_off = np.ascontiguousarray(rec_off, np.uint64)
+    nbytes = int(rec_off[-1]) if n >= 0 else 0
+    meta = np.zeros(max(n, 1), META_DTYPE)
+    info = np.zeros(max(n, 1), INFO_DTYPE)
+    acl = np.zeros(max(nbytes, 1), ACL_DTYPE)
+    reg = np.zeros(max(nbytes, 1), np.uint32)
+    data = np.zeros(nbytes + 16 * n + 16, np.uint8) if materialize else None
+    totals = np.zeros(3, np.uint64)
+    lib.oracle_decode_batch(_p(rec), _p(rec_off), n, _p(meta), _p(info), _p(acl), len(acl),
+                            _p(reg), len(reg), _p(data), 0 if data is None else len(data),
+                            _p(totals))
+    return (meta[:n], info[:n], acl[: int(totals[0])], reg[: int(totals[1])],
+            None if data is None else data[: int(totals[2])], totals)
+
+
+def key(row, meta_status: int):
+    out = (C.c_uint8 * 29)()
+    row = np.ascontiguousarray(row)
+    st = load().oracle_key(_p(row), meta_status, out)
+    return st, bytes(out)

@@ -1,0 +1,271 @@
+"""Parity of the gfx950 path (through the C ABI) with the CPU oracle.
+
+Bit-exact: encoded record bytes, offsets and statuses; decoded rows, record
+info, ACL/region tables, materialised payloads and keys — on generated batches
+of every benchmark shape, on the reference's fixture, on the reference's
+decoder error vectors and on a fuzzed corpus of malformed records. Full-size
+batches are checked through size-independent properties (payload digests
+survive encode -> decode; a sample of records equals the oracle's bytes).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from fixtures import load_object_fixture, py_uvarint  # noqa: E402
+from honu_amd import object as hobj  # noqa: E402
+from honu_amd.metadata import META_DTYPE, normalize, pack_batch, unpack_row  # noqa: E402
+from honu_amd.workload import gen_host_batch, gen_meta  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def codec():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    c = hobj.Codec(0, 1 << 16)
+    yield c
+    c.close()
+
+
+def dev(a, codec):
+    return hobj._dev_bytes(np.ascontiguousarray(a), codec.torch_device)
+
+
+def gpu_marshal(codec, hb):
+    r = codec.marshal(hobj.DeviceBatch.from_host(hb, codec.torch_device))
+    torch.cuda.synchronize()
+    return r.host()
+
+
+def gpu_decode(codec, rec, off, materialize=False):
+    n = len(off) - 1
+    d = codec.decode(dev(rec if len(rec) else np.zeros(1, np.uint8), codec), dev(off, codec), n,
+                     materialize=materialize, rec_bytes=int(off[-1]))
+    torch.cuda.synchronize()
+    return d.host()
+
+
+def assert_decode_equal(oracle_lib, codec, rec, off, materialize=False):
+    meta, info, acl, reg, data, tot = gpu_decode(codec, rec, off, materialize)
+    ometa, oinfo, oacl, oreg, odata, otot = oracle_lib.decode_batch(rec, off, materialize)
+    n = len(off) - 1
+    assert np.array_equal(tot, otot)
+    assert info.tobytes() == oinfo.tobytes()
+    bad = [i for i in range(n) if meta[i].tobytes() != ometa[i].tobytes()]
+    assert not bad, (bad[:5], meta[bad[0]], ometa[bad[0]])
+    assert acl.tobytes() == oacl.tobytes()
+    assert reg.tobytes() == oreg.tobytes()
+    if materialize:
+        for i in range(n):
+            if oinfo[i]["data_status"] == 0 and oinfo[i]["data_len"]:
+                o, ln = int(oinfo[i]["data_off"]), int(oinfo[i]["data_len"])
+                assert data[o:o + ln].tobytes() == odata[o:o + ln].tobytes(), i
+    return meta, info, acl, reg, data
+
+
+# --------------------------------------------------------------------------
+def test_fixture_object(codec, oracle_lib):
+    """TestObject (object_test.go:23-45) through the GPU."""
+    meta, data = load_object_fixture()
+    obj = hobj.Marshal(meta, data)
+    assert len(obj) == 1264
+    out, off, st = oracle_lib.marshal_batch(pack_batch([meta], [data]))
+    assert bytes(obj) == out.tobytes()
+    assert obj.StorageVersion() == 1
+    assert obj.Metadata() == normalize(meta)
+    assert obj.Data() == data
+    assert obj.Tombstone() is False
+    key = obj.Key()
+    assert key == bytes([1]) + bytes(16) + (12).to_bytes(8, "big") + (8).to_bytes(4, "big")
+    tomb = hobj.Marshal(meta, None)
+    assert tomb.Tombstone() is True and tomb.Data() is None
+
+
+def test_nil_and_malformed_objects(codec):
+    """TestNil / TestMalformed (object_test.go:60-83)."""
+    with pytest.raises(hobj.ErrBadVersion):
+        hobj.Object(b"").Metadata()
+    with pytest.raises(hobj.ErrBadVersion):
+        hobj.Object(b"").Data()
+    assert hobj.Object(b"").Tombstone() is False
+    with pytest.raises(hobj.ErrMalformed):
+        hobj.Object(b"\x01").Metadata()
+    with pytest.raises(hobj.ErrMalformed):
+        hobj.Object(b"\x01").Data()
+    with pytest.raises(hobj.GoPanic):
+        hobj.Marshal(None, b"x")
+
+
+@pytest.mark.parametrize("shape,n", [("small", 3000), ("medium", 500), ("large", 96),
+                                     ("xlarge", 6), ("mixed", 800)])
+def test_encode_parity(codec, oracle_lib, shape, n):
+    hb = gen_host_batch(21, shape, 5000, n)
+    out, off, st = gpu_marshal(codec, hb)
+    oout, ooff, ost = oracle_lib.marshal_batch(hb)
+    assert np.array_equal(st, ost) and (st == 0).all()
+    assert np.array_equal(off, ooff)
+    assert out.tobytes() == oout.tobytes()
+
+
+@pytest.mark.parametrize("materialize", [False, True])
+@pytest.mark.parametrize("shape,n", [("small", 3000), ("large", 64), ("mixed", 600)])
+def test_decode_parity(codec, oracle_lib, shape, n, materialize):
+    hb = gen_host_batch(22, shape, 0, n)
+    rec, off, st = oracle_lib.marshal_batch(hb)
+    meta, info, acl, reg, data = assert_decode_equal(oracle_lib, codec, rec, off, materialize)
+    assert (info["meta_status"] == 0).all()
+    for i in range(0, n, max(1, n // 50)):
+        src = normalize(unpack_row(hb.meta[i], hb.var, hb.acl, hb.regions))
+        assert unpack_row(meta[i], rec, acl, reg) == src
+
+
+def _tail_record(tail):
+    return b"\x01\x00" + tail
+
+
+def malformed_corpus(oracle_lib, seed=5):
+    """Reference decoder vectors + truncations + byte flips of valid records."""
+    rng = np.random.default_rng(seed)
+    base = b"\x01" + bytes(32) + b"\x00\x00\x00" + bytes(32) + b"\x07"
+    objs = [b"", b"\x01", b"\x01\x00", b"\x01\x00\x00", b"\x01\x80\x01", b"\x02\x00\x00",
+            b"\x01\x00\xf2", b"\x01\x05\x00\x00", b"\x01" + b"\xff" * 9 + b"\x01\x00",
+            _tail_record(b"\x01"), _tail_record(b"\x01" + bytes(5)),
+            _tail_record(base + py_uvarint(2**45 + 1)), _tail_record(base + py_uvarint(2**45)),
+            _tail_record(base + b"\x00" + py_uvarint(2**46 + 1)),
+            _tail_record(base + b"\x00\x01\xff\xff\xff\xff\x7f" + bytes(7)),
+            _tail_record(base + b"\x00\x01\xff\xff\xff\xff\xff\x01" + bytes(7))]
+    for fr in (b"", b"\xff\xff", b"\xff\x12\x23\x42\xf2\x21", b"\x00", b"\x05abc",
+               b"\xff" * 9 + b"\x7f", b"\xff" * 9 + b"\x01", b"\xff" * 8 + b"\x7f",
+               b"\xff" * 7 + b"\x7f"):
+        objs.append(_tail_record(b"\x01" + bytes(32) + b"\x00\x00" + fr))
+    hb = gen_host_batch(9, "small", 0, 24)
+    rec, off, _ = oracle_lib.marshal_batch(hb)
+    valid = [rec[int(off[i]):int(off[i + 1])].tobytes() for i in range(24)]
+    meta, _ = load_object_fixture()
+    fx = oracle_lib.marshal_batch(pack_batch([meta], [b"xyz"]))[0].tobytes()
+    valid.append(fx)
+    for v in valid[:4] + [fx]:  # every truncation point of the metadata tail
+        for cut in range(0, len(v), 1 if len(v) < 2000 else 7):
+            objs.append(v[:cut])
+    for v in valid:
+        for _ in range(40):
+            b = bytearray(v)
+            for _k in range(int(rng.integers(1, 4))):
+                pos = int(rng.integers(0, len(b)))
+                b[pos] = int(rng.integers(0, 256))
+            objs.append(bytes(b))
+    for _ in range(200):
+        objs.append(rng.integers(0, 256, int(rng.integers(0, 64)), dtype=np.uint8).tobytes())
+    return objs
+
+
+def test_malformed_corpus_parity(codec, oracle_lib):
+    objs = malformed_corpus(oracle_lib)
+    off = np.zeros(len(objs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(o) for o in objs])
+    rec = np.frombuffer(b"".join(objs) + b"\0", np.uint8)[: int(off[-1])]
+    meta, info, *_ = assert_decode_equal(oracle_lib, codec, rec, off, materialize=True)
+    statuses = set(info["meta_status"].tolist())
+    assert {0, 1, 2, 3, 4, 5, 6, 7, 8} <= statuses, statuses
+
+
+def test_keys_parity(codec, oracle_lib):
+    hb = gen_host_batch(23, "small", 0, 500)
+    rec, off, _ = oracle_lib.marshal_batch(hb)
+    objs = [rec[int(off[i]):int(off[i + 1])].tobytes() for i in range(500)] + [b"\x01\x00\x00", b""]
+    off2 = np.zeros(len(objs) + 1, np.uint64)
+    off2[1:] = np.cumsum([len(o) for o in objs])
+    rec2 = np.frombuffer(b"".join(objs), np.uint8)
+    d = codec.decode(dev(rec2, codec), dev(off2, codec), len(objs), rec_bytes=int(off2[-1]))
+    keys, kst = codec.keys(d)
+    torch.cuda.synchronize()
+    keys = hobj._to_host(keys, 29 * len(objs), np.uint8).reshape(-1, 29)
+    kst = hobj._to_host(kst, 4 * len(objs), np.int32)
+    meta, info, *_ = d.host()
+    for i in range(len(objs)):
+        st, k = oracle_lib.key(meta[i:i + 1], int(info[i]["meta_status"]))
+        assert st == kst[i] and (st != 0 or k == keys[i].tobytes()), i
+    assert kst[-2] == 8 and kst[-1] == 1  # nil Version panics; empty object: ErrBadVersion
+
+
+def test_encode_input_errors(codec, oracle_lib):
+    meta, data = load_object_fixture()
+    hb = pack_batch([meta, None, meta, meta], [data, b"a", b"", data])
+    hb.meta[2]["mime"]["off"] = 10**9          # span outside the var arena
+    hb.meta[3]["acl_count"] = 10**6            # list outside the ACL table
+    out, off, st = gpu_marshal(codec, hb)
+    oout, ooff, ost = oracle_lib.marshal_batch(hb)
+    assert st.tolist() == ost.tolist() == [0, 8, 10, 10]
+    assert np.array_equal(off, ooff) and out.tobytes() == oout.tobytes()
+
+
+def test_decode_capacity(codec, oracle_lib):
+    hb = gen_host_batch(24, "small", 0, 64)
+    rec, off, _ = oracle_lib.marshal_batch(hb)
+    n = 64
+    d = codec.decode(dev(rec, codec), dev(off, codec), n, materialize=True, acl_cap=10,
+                     regions_cap=10, data_cap=4096, rec_bytes=int(off[-1]))
+    torch.cuda.synchronize()
+    meta, info, acl, reg, data, tot = d.host()
+    assert int(tot[0]) > 10 and int(tot[2]) > 4096
+    assert (info["meta_status"] == 9).any() and (info["data_status"] == 9).any()
+    ok = info["data_status"] == 0
+    assert (info["data_off"][ok] + info["data_len"][ok] <= 4096).all()
+
+
+def test_device_payload_and_digest(codec):
+    meta, var, acl, reg, off = gen_meta(31, "mixed", 77, 300)
+    hb = gen_host_batch(31, "mixed", 77, 300)
+    d_off = dev(off, codec)
+    d_pay = codec._empty(int(off[-1]))
+    hobj._lib.check(codec.lib.honu_gen_payload(codec.ctx, 31, 77, 300, hobj._lib.ptr(d_off),
+                                               hobj._lib.ptr(d_pay), codec.stream), "gen")
+    dig = codec._empty(8 * 300)
+    hobj._lib.check(codec.lib.honu_digest_records(codec.ctx, hobj._lib.ptr(d_pay),
+                                                  hobj._lib.ptr(d_off), 0, 300,
+                                                  hobj._lib.ptr(dig), codec.stream), "digest")
+    torch.cuda.synchronize()
+    pay = hobj._to_host(d_pay, int(off[-1]), np.uint8)
+    assert pay.tobytes() == hb.payload[: int(off[-1])].tobytes()
+    from honu_amd.workload import digest_host
+    dg = hobj._to_host(dig, 8 * 300, np.uint64)
+    for i in range(0, 300, 7):
+        assert int(dg[i]) == digest_host(pay[int(off[i]):int(off[i + 1])].tobytes())
+
+
+def test_full_size_property_large(codec, oracle_lib):
+    """4096 Large records (~0.8 GB) generated on the device: payload digests
+    survive encode -> materialising decode; sampled records equal the oracle's."""
+    n = 4096
+    meta, var, acl, reg, off = gen_meta(41, "large", 0, n)
+    D = lambda a: dev(a, codec)  # noqa: E731
+    db = hobj.DeviceBatch(D(meta), D(var), len(var), D(acl), len(acl), D(reg), len(reg),
+                          codec._empty(int(off[-1])), D(off), n)
+    L = hobj._lib
+    L.check(codec.lib.honu_gen_payload(codec.ctx, 41, 0, n, L.ptr(db.payload_off),
+                                       L.ptr(db.payload), codec.stream), "gen")
+    enc = codec.marshal(db)
+    dec = codec.decode(enc.out, enc.out_off, n, materialize=True)
+    lens = torch.from_numpy(np.diff(off).astype(np.uint64).view(np.int64)).to(codec.torch_device)
+    dsrc, ddst = codec._empty(8 * n), codec._empty(8 * n)
+    L.check(codec.lib.honu_digest_records(codec.ctx, L.ptr(db.payload), L.ptr(db.payload_off), 0,
+                                          n, L.ptr(dsrc), codec.stream), "digest")
+    info_t = dec.info.view(torch.int64)[: 4 * n].view(n, 4)
+    doff = info_t[:, 0].contiguous()
+    dlen = info_t[:, 1].contiguous()
+    L.check(codec.lib.honu_digest_records(codec.ctx, L.ptr(dec.data), L.ptr(doff), L.ptr(dlen), n,
+                                          L.ptr(ddst), codec.stream), "digest")
+    torch.cuda.synchronize()
+    assert torch.equal(dlen.cpu(), lens.cpu())
+    assert torch.equal(dsrc[: 8 * n].cpu(), ddst[: 8 * n].cpu())
+    _, info, *_ = dec.host()
+    assert (info["meta_status"] == 0).all() and (info["data_status"] == 0).all()
+    sample = [0, 1, 17, 1023, 2048, n - 1]
+    hb = gen_host_batch(41, "large", 0, n)
+    oout, ooff, _ = oracle_lib.marshal_batch(hb)
+    out, goff, _ = enc.host()
+    assert np.array_equal(goff, ooff)
+    for i in sample:
+        assert out[int(goff[i]):int(goff[i + 1])].tobytes() == oout[int(ooff[i]):int(ooff[i + 1])].tobytes()

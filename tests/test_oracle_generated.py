@@ -1,0 +1,58 @@
+"""Round trips of generated batches of every benchmark shape through the CPU
+oracle, cross-checked record by record against the independent pure-Python
+encoder (tests/fixtures.py). CPU only."""
+import numpy as np
+import pytest
+
+from fixtures import py_marshal
+from honu_amd.metadata import normalize, unpack_row
+from honu_amd.workload import digest_host, gen_host_batch
+
+
+@pytest.mark.parametrize("shape,n", [("small", 200), ("medium", 60), ("large", 12),
+                                     ("xlarge", 2), ("mixed", 100)])
+def test_generated_roundtrip(oracle_lib, shape, n):
+    hb = gen_host_batch(11, shape, 1000, n)
+    out, off, st = oracle_lib.marshal_batch(hb)
+    assert (st == 0).all()
+    for i in range(min(n, 40)):
+        m = unpack_row(hb.meta[i], hb.var, hb.acl, hb.regions)
+        d = bytes(hb.payload[int(hb.payload_off[i]):int(hb.payload_off[i + 1])])
+        assert bytes(out[int(off[i]):int(off[i + 1])]) == py_marshal(m, d), i
+    meta, info, acl, reg, data, tot = oracle_lib.decode_batch(out, off, materialize=True)
+    assert (info["meta_status"] == 0).all() and (info["data_status"] == 0).all()
+    for i in range(n):
+        src = normalize(unpack_row(hb.meta[i], hb.var, hb.acl, hb.regions))
+        assert unpack_row(meta[i], out, acl, reg) == src, i
+        dl = int(info[i]["data_len"])
+        assert dl == int(hb.payload_off[i + 1] - hb.payload_off[i])
+        got = bytes(data[int(info[i]["data_off"]):int(info[i]["data_off"]) + dl])
+        assert got == bytes(hb.payload[int(hb.payload_off[i]):int(hb.payload_off[i + 1])])
+        assert int(info[i]["data_off"]) % 16 == 0
+
+
+def test_generator_distributions():
+    """Shape of the generated metadata follows object_test.go:195-386."""
+    hb = gen_host_batch(3, "small", 0, 4000)
+    m = hb.meta
+    lens = np.diff(hb.payload_off.astype(np.int64))
+    assert lens.min() >= 512 and lens.max() < 4608
+    acl = m["acl_count"]
+    assert acl.max() <= 64 and 0.05 < (acl == 0).mean() < 0.15
+    regs = m["regions_count"]
+    assert regs.max() <= 9 and 0.05 < (regs == 0).mean() < 0.15
+    assert 0.85 < ((m["present"] & 4) != 0).mean() < 0.95          # Parent p=.9
+    assert 0.20 < (m["tombstone"] == 1).mean() < 0.30               # Tombstone p=.25
+    assert (m["permissions"] < 255).all() and (m["flags"] < 255).all()
+    lg = gen_host_batch(3, "large", 0, 50)
+    ll = np.diff(lg.payload_off.astype(np.int64))
+    assert ll.min() >= 65536 and ll.max() < 327680
+
+
+def test_digest_host_properties():
+    a = bytes(range(256)) * 3
+    assert digest_host(a) == digest_host(bytes(a))
+    assert digest_host(a) != digest_host(a[:-1])
+    b = bytearray(a)
+    b[100], b[101] = b[101], b[100]
+    assert digest_host(a) != digest_host(bytes(b))
