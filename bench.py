@@ -1,0 +1,368 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident encode + decode of a 1M-record Large batch per GPU.
+
+One step = object.Marshal of every record of the batch (object.go:24-45) followed
+by Object.Metadata() + Object.Data() of every encoded record (object.go:66-99)
+with the payloads materialised into a packed arena, all on the GPU through the
+C ABI (include/honu_codec.h). Inputs (metadata rows + arenas + payload arena)
+are resident in HBM before the timed region. 1M Large records in + out do not
+fit one MI355X (≈197.6 GB of payload, ≈395 GB per direction pair), so the batch
+is processed as device-resident chunks of --chunk records whose output buffers
+are reused; every byte of every record is encoded and decoded each step.
+
+Multi-GPU: weak scaling, one process per GPU (torchrun), each rank encodes and
+decodes its own shard of --records records (records are independent: no
+data-path collective). A barrier + synchronize brackets the timed steps and the
+max time over ranks is reported.
+
+Prints ONE JSON line on rank 0 (see DESIGN.md for every field).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from honu_amd import _lib  # noqa: E402
+from honu_amd.object import Codec  # noqa: E402
+from honu_amd.workload import gen_meta, shape_id  # noqa: E402
+
+METRIC = "GiB/s + records/s device-resident encode+decode, 1M Large(~300KB) object batch"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse_args():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--records", type=int, default=1 << 20, help="records per GPU")
+    p.add_argument("--shape", default="large")
+    p.add_argument("--chunk", type=int, default=1 << 16)
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-records", type=int, default=2048)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-verify", action="store_true")
+    return p.parse_args()
+
+
+def P(t):
+    return t.data_ptr()
+
+
+class Bench:
+    def __init__(self, args, rank, device):
+        self.args = args
+        self.dev = torch.device("cuda", device)
+        self.codec = Codec(device, max_records=args.chunk)
+        self.lib = self.codec.lib
+        N = args.records
+        self.N = N
+        self.first = rank * N
+        t0 = time.time()
+        meta, var, acl, reg, off = gen_meta(args.seed, args.shape, self.first, N)
+        self.host_meta = meta
+        self.host_off = off
+        self.gen_s = time.time() - t0
+
+        def D(a):
+            a = np.ascontiguousarray(a)
+            t = torch.empty(max(a.nbytes, 16), dtype=torch.uint8, device=self.dev)
+            if a.nbytes:
+                t[: a.nbytes].copy_(torch.from_numpy(a.view(np.uint8).reshape(-1)))
+            return t
+
+        self.meta, self.var, self.acl, self.reg, self.off = D(meta), D(var), D(acl), D(reg), D(off)
+        self.var_len, self.acl_len, self.reg_len = len(var), len(acl), len(reg)
+        self.payload_bytes = int(off[N])
+        self.payload = torch.empty(self.payload_bytes + 16, dtype=torch.uint8, device=self.dev)
+        _lib.check(self.lib.honu_gen_payload(self.codec.ctx, args.seed, self.first, N, P(self.off),
+                                             P(self.payload), self.stream), "gen_payload")
+        self.chunks = [(a, min(a + args.chunk, N)) for a in range(0, N, args.chunk)]
+        C = args.chunk
+        self.out_off = torch.empty(8 * (C + 1), dtype=torch.uint8, device=self.dev)
+        self.status = torch.empty(4 * C + 16, dtype=torch.uint8, device=self.dev)
+        # sizing pass (untimed): exact record bytes of every chunk
+        self.rec_bytes = []
+        for a, b in self.chunks:
+            self._sizes(a, b)
+            self.rec_bytes.append(int(self.out_off.view(torch.int64)[b - a].item()))
+        self.total_rec_bytes = sum(self.rec_bytes)
+        lens = np.diff(off.astype(np.int64))
+        acl_n = meta["acl_count"].astype(np.int64)
+        reg_n = meta["regions_count"].astype(np.int64)
+        alloc = (lens + 15) // 16 * 16
+        self.chunk_payload = [int(lens[a:b].sum()) for a, b in self.chunks]
+        self.acl_cap = max(int(acl_n[a:b].sum()) for a, b in self.chunks) + 1
+        self.reg_cap = max(int(reg_n[a:b].sum()) for a, b in self.chunks) + 1
+        self.data_cap = max(int(alloc[a:b].sum()) for a, b in self.chunks) + 16
+        self.out_cap = max(self.rec_bytes) + 16
+        self.out = torch.empty(self.out_cap, dtype=torch.uint8, device=self.dev)
+        self.dmeta = torch.empty(352 * C, dtype=torch.uint8, device=self.dev)
+        self.dinfo = torch.empty(32 * C, dtype=torch.uint8, device=self.dev)
+        self.dacl = torch.empty(20 * self.acl_cap, dtype=torch.uint8, device=self.dev)
+        self.dreg = torch.empty(4 * self.reg_cap, dtype=torch.uint8, device=self.dev)
+        self.data = torch.empty(self.data_cap, dtype=torch.uint8, device=self.dev)
+        self.totals = torch.empty(32, dtype=torch.uint8, device=self.dev)
+        self.events = None
+        torch.cuda.synchronize()
+
+    @property
+    def stream(self):
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    def _sizes(self, a, b):
+        n = b - a
+        L, c, s = self.lib, self.codec.ctx, self.stream
+        _lib.check(L.honu_encode_sizes(c, P(self.meta) + 352 * a, self.var_len, P(self.acl),
+                                       self.acl_len, P(self.reg), self.reg_len, P(self.off) + 8 * a,
+                                       n, P(self.out_off), P(self.status), s), "sizes")
+        _lib.check(L.honu_exclusive_scan(c, P(self.out_off), n, P(self.out_off), s), "scan")
+
+    def _ev(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def step(self, timed=False):
+        L, c = self.lib, self.codec.ctx
+        for a, b in self.chunks:
+            n = b - a
+            s = self.stream
+            self._sizes(a, b)
+            _lib.check(L.honu_encode_records(c, P(self.meta) + 352 * a, P(self.var), P(self.acl),
+                                             P(self.reg), P(self.off) + 8 * a, n, P(self.out),
+                                             self.out_cap, P(self.out_off), P(self.status), s),
+                       "encode_records")
+            e0 = self._ev() if timed else None
+            _lib.check(L.honu_encode_payloads(c, P(self.payload), P(self.off) + 8 * a, n,
+                                              P(self.out), P(self.out_off), P(self.status), s),
+                       "encode_payloads")
+            e1 = self._ev() if timed else None
+            _lib.check(L.honu_decode_parse(c, P(self.out), P(self.out_off), n, P(self.dmeta),
+                                           P(self.dinfo), s), "decode_parse")
+            _lib.check(L.honu_decode_tables(c, P(self.out), n, P(self.dmeta), P(self.dinfo),
+                                            P(self.dacl), self.acl_cap, P(self.dreg), self.reg_cap,
+                                            P(self.data), self.data_cap, P(self.totals), s),
+                       "decode_tables")
+            e2 = self._ev() if timed else None
+            _lib.check(L.honu_decode_payloads(c, P(self.out), n, P(self.dinfo), P(self.data),
+                                              P(self.totals), s), "decode_payloads")
+            e3 = self._ev() if timed else None
+            if timed:
+                self.events.append((a, b, e0, e1, e2, e3))
+
+    def verify(self):
+        """Size-independent checks on the last chunk of the last step: every
+        status is OK, every decoded payload digest equals its source digest,
+        and sampled decoded rows equal the input rows."""
+        L, c, s = self.lib, self.codec.ctx, self.stream
+        a, b = self.chunks[-1]
+        n = b - a
+        st = self.status[: 4 * n].view(torch.int32)
+        info = self.dinfo[: 32 * n].view(torch.int64).view(n, 4)
+        ms = info[:, 2].contiguous().view(torch.int32)
+        dsrc = torch.empty(8 * n, dtype=torch.uint8, device=self.dev)
+        ddst = torch.empty(8 * n, dtype=torch.uint8, device=self.dev)
+        _lib.check(L.honu_digest_records(c, P(self.payload), P(self.off) + 8 * a, 0, n, P(dsrc), s),
+                   "digest")
+        doff, dlen = info[:, 0].contiguous(), info[:, 1].contiguous()
+        _lib.check(L.honu_digest_records(c, P(self.data), P(doff), P(dlen), n, P(ddst), s), "digest")
+        torch.cuda.synchronize()
+        ok = bool((st == 0).all()) and bool((ms == 0).all())
+        ok &= torch.equal(dsrc, ddst)
+        exp_len = torch.from_numpy(np.diff(self.host_off[a:b + 1].astype(np.int64))).to(self.dev)
+        ok &= torch.equal(dlen, exp_len)
+        rows = self.dmeta[: 352 * n].cpu().numpy().view(self.host_meta.dtype)
+        src = self.host_meta[a:b]
+        for f in ("present", "pid", "vid", "region", "created", "modified", "acl_count",
+                  "regions_count", "permissions", "flags", "owner", "group"):
+            got, exp = rows[f], src[f]
+            if f == "present":  # decode adds REGIONS_NONNIL
+                got = got & ~np.uint32(0x80)
+            ok &= bool(np.array_equal(got, exp))
+        return bool(ok)
+
+
+def copy_peak_gbs(dev, nbytes=8 << 30, reps=5):
+    """Achievable HBM copy rate on this device (torch copy_), read+write bytes."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / reps
+    del a, b
+    torch.cuda.empty_cache()
+    return 2 * nbytes / t / 1e9
+
+
+def cpu_baseline(args):
+    """The CPU oracle (plain-C restatement of the Go path, 1 thread) on a bounded
+    sample of the same workload, cycled for >= --cpu-seconds."""
+    sys.path.insert(0, ROOT)
+    from honu_amd.metadata import HostBatch
+    from oracle import oracle
+
+    n = args.cpu_records
+    meta, var, acl, reg, off = gen_meta(args.seed, args.shape, 0, n)
+    rng = np.random.default_rng(args.seed)
+    payload = rng.integers(0, 256, int(off[n]) + 1, dtype=np.uint8)
+    hb = HostBatch(meta, var, acl, reg, payload, off)
+    rec_bytes = 0
+    t0 = time.perf_counter()
+    iters = 0
+    while True:
+        out, ooff, st = oracle.marshal_batch(hb)
+        oracle.decode_batch(out, ooff, materialize=True)
+        rec_bytes += int(ooff[-1])
+        iters += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds:
+            break
+    model = ""
+    try:
+        model = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if "model name" in ln][0]
+    except Exception:
+        pass
+    return {
+        "value": rec_bytes / el / 2**30,
+        "unit": "GiB/s",
+        "records_per_s": iters * n / el,
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{n} {args.shape} records ({int(ooff[-1]) / 1e9:.2f} GB encoded) encoded + "
+                  f"decoded (materialising) {iters}x in {el:.1f} s by the C oracle, 1 thread, {model}; "
+                  "no Go toolchain on the box, so the Go reference itself cannot be timed",
+    }
+
+
+def main():
+    args = parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    bench = Bench(args, rank, local)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        bench.step()
+    torch.cuda.synchronize()
+    bench.events = []
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        bench.step(timed=True)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=bench.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-launch kernel times of the two payload-copy kernels (the HBM-bound part)
+    enc_ms = [e0.elapsed_time(e1) for (_, _, e0, e1, _, _) in bench.events]
+    dec_ms = [e2.elapsed_time(e3) for (_, _, _, _, e2, e3) in bench.events]
+    enc_bytes = [2 * bench.chunk_payload[i % len(bench.chunks)] for i in range(len(enc_ms))]
+    enc_gbs = sum(enc_bytes) / (sum(enc_ms) / 1e3) / 1e9
+    dec_gbs = sum(enc_bytes) / (sum(dec_ms) / 1e3) / 1e9
+    verified = None if args.no_verify else bench.verify()
+    ok_all = verified
+    if dist is not None and verified is not None:
+        v = torch.tensor([1 if verified else 0], device=bench.dev)
+        dist.all_reduce(v, op=dist.ReduceOp.MIN)
+        ok_all = bool(v.item())
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    step_s = elapsed / args.steps
+    total_records = bench.N * world
+    total_bytes = bench.total_rec_bytes * world
+    launches = len(dec_ms)
+    dom_ms, dom_gbs, dom_name = (sum(dec_ms), dec_gbs, "k_copy_segments<DecodeSegments>")
+    if sum(enc_ms) > sum(dec_ms):
+        dom_ms, dom_gbs, dom_name = (sum(enc_ms), enc_gbs, "k_copy_segments<EncodeSegments>")
+    peak_meas = copy_peak_gbs(bench.dev)
+    result = {
+        "metric": METRIC,
+        "value": total_bytes / step_s / 2**30,
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": step_s * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: seeded generator mirroring object_test.go:195-386, payload bytes "
+                "generated on device",
+        "config": {
+            "workload": f"{bench.N} {args.shape} records per GPU: encode (object.Marshal) + "
+                        "materialising decode (Object.Metadata + Object.Data)",
+            "records_per_gpu": bench.N,
+            "shape": args.shape,
+            "chunk_records": args.chunk,
+            "encoded_bytes_per_gpu": bench.total_rec_bytes,
+            "payload_bytes_per_gpu": bench.payload_bytes,
+            "parallelism": f"dp{world} (records sharded, no data-path collective)",
+        },
+        "records_per_s": total_records / step_s,
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom_name,
+            "achieved": dom_gbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": dom_gbs / HBM_PEAK_GBS,
+            "traffic": None,
+            "launches": launches,
+            "avg_launch_ms": dom_ms / launches,
+            "algorithmic_bytes_per_launch": sum(enc_bytes) / launches,
+        },
+        "kernels": {
+            "encode_copy_gbs": enc_gbs,
+            "decode_copy_gbs": dec_gbs,
+            "encode_copy_ms_per_step": sum(enc_ms) / args.steps,
+            "decode_copy_ms_per_step": sum(dec_ms) / args.steps,
+            "step_hbm_gbs_algorithmic": 4 * bench.total_rec_bytes / step_s / 1e9,
+            "copy_peak_measured_gbs": peak_meas,
+        },
+        "verified": ok_all,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args)
+    print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

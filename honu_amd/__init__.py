@@ -13,6 +13,7 @@ from .metadata import (AccessControl, Compression, Encryption, Metadata, Publish
 
 def __getattr__(name):  # object API loads the HIP library lazily
     if name in ("object", "Codec", "Marshal", "Object", "marshal_batch", "decode_batch"):
-        from . import object as _object
+        import importlib
+        _object = importlib.import_module(__name__ + ".object")
         return _object if name == "object" else getattr(_object, name)
     raise AttributeError(name)

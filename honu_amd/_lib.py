@@ -33,6 +33,10 @@ _PROTOS = {
     "honu_encode_sizes": (I32, [P, P, U64, P, U64, P, U64, P, U64, P, P, P]),
     "honu_exclusive_scan": (I32, [P, P, U64, P, P]),
     "honu_encode": (I32, [P, P, P, U64, P, U64, P, U64, P, P, U64, P, U64, P, P, P]),
+    "honu_encode_records": (I32, [P, P, P, P, P, P, U64, P, U64, P, P, P]),
+    "honu_encode_payloads": (I32, [P, P, P, U64, P, P, P, P]),
+    "honu_decode_tables": (I32, [P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),
+    "honu_decode_payloads": (I32, [P, P, U64, P, P, P, P]),
     "honu_marshal_batch": (I32, [P, P, P, U64, P, U64, P, U64, P, P, U64, P, U64, P, P, P]),
     "honu_decode_parse": (I32, [P, P, P, U64, P, P, P]),
     "honu_decode_fill": (I32, [P, P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),

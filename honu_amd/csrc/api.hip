@@ -162,6 +162,32 @@ int32_t honu_exclusive_scan(honu_ctx *ctx, const uint64_t *d_in, uint64_t n, uin
     return HONU_OK;
 }
 
+int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
+                            const honu_acl *d_acl, const uint32_t *d_regions,
+                            const uint64_t *d_payload_off, uint64_t n, uint8_t *d_out,
+                            uint64_t out_cap, const uint64_t *d_out_off, int32_t *d_status,
+                            void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n && (!d_meta || !d_payload_off || !d_out || !d_out_off || !d_status))
+        return arg_fail("null pointer");
+    if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_encode_meta(ctx->geom, d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
+                              out_cap, d_out_off, d_status, (hipStream_t)stream));
+    return HONU_OK;
+}
+
+int32_t honu_encode_payloads(honu_ctx *ctx, const uint8_t *d_payload, const uint64_t *d_payload_off,
+                             uint64_t n, uint8_t *d_out, const uint64_t *d_out_off,
+                             const int32_t *d_status, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n && (!d_payload_off || !d_out || !d_out_off || !d_status)) return arg_fail("null pointer");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_encode_copy(ctx->geom, d_payload, d_payload_off, n, d_out, d_out_off, d_status,
+                              (hipStream_t)stream));
+    return HONU_OK;
+}
+
 int32_t honu_encode(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var, uint64_t var_len,
                     const honu_acl *d_acl, uint64_t acl_len, const uint32_t *d_regions,
                     uint64_t regions_len, const uint8_t *d_payload, const uint64_t *d_payload_off,
@@ -170,16 +196,11 @@ int32_t honu_encode(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var
     (void)var_len;
     (void)acl_len;
     (void)regions_len;
-    if (!ctx) return arg_fail("ctx");
-    if (n && (!d_meta || !d_payload_off || !d_out || !d_out_off || !d_status))
-        return arg_fail("null pointer");
-    if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
-    HIPCHK(hipSetDevice(ctx->device));
-    hipStream_t s = (hipStream_t)stream;
-    HIPCHK(launch_encode_meta(ctx->geom, d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
-                              out_cap, d_out_off, d_status, s));
-    HIPCHK(launch_encode_copy(ctx->geom, d_payload, d_payload_off, n, d_out, d_out_off, d_status, s));
-    return HONU_OK;
+    int32_t st = honu_encode_records(ctx, d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
+                                     out_cap, d_out_off, d_status, stream);
+    if (st) return st;
+    return honu_encode_payloads(ctx, d_payload, d_payload_off, n, d_out, d_out_off, d_status,
+                                stream);
 }
 
 int32_t honu_marshal_batch(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
@@ -213,12 +234,10 @@ int32_t honu_decode_parse(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
     return HONU_OK;
 }
 
-int32_t honu_decode_fill(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
-                         uint64_t n, honu_meta *d_meta, honu_record_info *d_info,
-                         honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
-                         uint64_t regions_cap, uint8_t *d_data, uint64_t data_cap,
-                         uint64_t *d_totals, void *stream) {
-    (void)d_rec_off;
+int32_t honu_decode_tables(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n, honu_meta *d_meta,
+                           honu_record_info *d_info, honu_acl *d_acl, uint64_t acl_cap,
+                           uint32_t *d_regions, uint64_t regions_cap, uint8_t *d_data,
+                           uint64_t data_cap, uint64_t *d_totals, void *stream) {
     if (!ctx) return arg_fail("ctx");
     if (n > ctx->max_n) return HONU_E_WORKSPACE;
     if (!aligned(d_acl, 4) || !aligned(d_regions, 4) || !aligned(d_data, 16))
@@ -232,9 +251,32 @@ int32_t honu_decode_fill(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_
     HIPCHK(launch_decode_fill(ctx->geom, d_rec, n, d_meta, d_info, ctx->scratch, ctx->counts,
                               ctx->offs, tot, d_acl, acl_cap, d_regions, regions_cap, d_data,
                               data_cap, s));
-    if (d_data)
-        HIPCHK(launch_decode_copy(ctx->geom, d_rec, n, d_info, ctx->scratch, ctx->offs, tot, d_data, s));
     return HONU_OK;
+}
+
+int32_t honu_decode_payloads(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n,
+                             const honu_record_info *d_info, uint8_t *d_data,
+                             const uint64_t *d_totals, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n > ctx->max_n) return HONU_E_WORKSPACE;
+    if (!d_data || !aligned(d_data, 16)) return arg_fail("data arena");
+    HIPCHK(hipSetDevice(ctx->device));
+    const uint64_t *tot = d_totals ? d_totals : ctx->totals;
+    HIPCHK(launch_decode_copy(ctx->geom, d_rec, n, d_info, ctx->scratch, ctx->offs, tot, d_data,
+                              (hipStream_t)stream));
+    return HONU_OK;
+}
+
+int32_t honu_decode_fill(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                         uint64_t n, honu_meta *d_meta, honu_record_info *d_info,
+                         honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
+                         uint64_t regions_cap, uint8_t *d_data, uint64_t data_cap,
+                         uint64_t *d_totals, void *stream) {
+    (void)d_rec_off;
+    int32_t st = honu_decode_tables(ctx, d_rec, n, d_meta, d_info, d_acl, acl_cap, d_regions,
+                                    regions_cap, d_data, data_cap, d_totals, stream);
+    if (st || !d_data) return st;
+    return honu_decode_payloads(ctx, d_rec, n, d_info, d_data, d_totals, stream);
 }
 
 int32_t honu_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,

@@ -102,7 +102,10 @@ def _dev_bytes(a: np.ndarray, device):
     a = np.ascontiguousarray(a)
     t = torch.empty(max(a.nbytes, 16), dtype=torch.uint8, device=device)
     if a.nbytes:
-        t[: a.nbytes].copy_(torch.from_numpy(a.view(np.uint8).reshape(-1)))
+        src = a.view(np.uint8).reshape(-1)
+        if not src.flags.writeable:
+            src = src.copy()
+        t[: a.nbytes].copy_(torch.from_numpy(src))
     return t
 
 

@@ -222,12 +222,23 @@ int32_t honu_exclusive_scan(honu_ctx *ctx, const uint64_t *d_in, uint64_t n, uin
  *   d_var, var_len:        byte arena indexed by honu_meta spans
  *   d_acl, acl_len:        ACL table indexed by acl_off/acl_count
  *   d_regions, regions_len: uint32 region table
- *   d_payload, d_payload_off: CSR payload arena (the `data` argument) */
+ *   d_payload, d_payload_off: CSR payload arena (the `data` argument)
+ * honu_encode = honu_encode_records (header + Metadata tail of every record)
+ * followed by honu_encode_payloads (the payload bytes, object.go:35); the two
+ * phases are exported separately so they can be scheduled and timed apart. */
 int32_t honu_encode(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var, uint64_t var_len,
                     const honu_acl *d_acl, uint64_t acl_len, const uint32_t *d_regions,
                     uint64_t regions_len, const uint8_t *d_payload, const uint64_t *d_payload_off,
                     uint64_t n, uint8_t *d_out, uint64_t out_cap, const uint64_t *d_out_off,
                     int32_t *d_status, void *stream);
+int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
+                            const honu_acl *d_acl, const uint32_t *d_regions,
+                            const uint64_t *d_payload_off, uint64_t n, uint8_t *d_out,
+                            uint64_t out_cap, const uint64_t *d_out_off, int32_t *d_status,
+                            void *stream);
+int32_t honu_encode_payloads(honu_ctx *ctx, const uint8_t *d_payload, const uint64_t *d_payload_off,
+                             uint64_t n, uint8_t *d_out, const uint64_t *d_out_off,
+                             const int32_t *d_status, void *stream);
 
 /* sizes + scan + encode in one call; d_out_off (n+1) is produced here. */
 int32_t honu_marshal_batch(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
@@ -249,16 +260,26 @@ int32_t honu_decode_parse(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
                           uint64_t n, honu_meta *d_meta, honu_record_info *d_info, void *stream);
 
 /* Phase 2: assign table offsets (exclusive scans over the counts), fill
- * the ACL and region tables, and when d_data != NULL materialise every
- * payload into d_data at 16-byte aligned offsets (d_info[i].data_off is then
- * relative to d_data). d_totals (device, 3 x u64) receives the totals the
- * batch needs: ACL entries, region entries, data-arena bytes. Records whose
+ * the ACL and region tables, and when d_data != NULL assign every payload a
+ * 16-byte aligned offset in d_data (d_info[i].data_off is then relative to
+ * d_data) and copy the payloads there (honu_decode_payloads). d_totals
+ * (device, 3 x u64) receives the totals the batch needs: ACL entries, region
+ * entries, data-arena bytes (the latter also in zero-copy mode). Records whose
  * outputs do not fit get HONU_ERR_CAPACITY in meta_status / data_status. */
 int32_t honu_decode_fill(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
                          uint64_t n, honu_meta *d_meta, honu_record_info *d_info,
                          honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
                          uint64_t regions_cap, uint8_t *d_data, uint64_t data_cap,
                          uint64_t *d_totals, void *stream);
+/* honu_decode_fill without the payload copy, and the copy alone (after
+ * honu_decode_tables with the same d_data and d_totals). */
+int32_t honu_decode_tables(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n, honu_meta *d_meta,
+                           honu_record_info *d_info, honu_acl *d_acl, uint64_t acl_cap,
+                           uint32_t *d_regions, uint64_t regions_cap, uint8_t *d_data,
+                           uint64_t data_cap, uint64_t *d_totals, void *stream);
+int32_t honu_decode_payloads(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n,
+                             const honu_record_info *d_info, uint8_t *d_data,
+                             const uint64_t *d_totals, void *stream);
 
 /* parse + fill in one call. */
 int32_t honu_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,

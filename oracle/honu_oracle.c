@@ -603,9 +603,13 @@ int oracle_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
             acl_pos += an;
             reg_pos += rn;
         }
-        if (data && info[i].data_status == HONU_OK && info[i].data_len) {
+        if (info[i].data_status == HONU_OK && info[i].data_len) {
             uint64_t dl = info[i].data_len;
             uint64_t src = info[i].data_off;
+            if (!data) { /* zero copy: only count the arena bytes a copy would need */
+                data_pos += (dl + 15) & ~15ull;
+                continue;
+            }
             info[i].data_off = data_pos;
             if (data_pos + dl > data_cap) {
                 info[i].data_status = HONU_ERR_CAPACITY;
