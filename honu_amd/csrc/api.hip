@@ -105,6 +105,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->geom.num_cu = prop.multiProcessorCount;
     c->geom.per_record_blocks = env_int("HONU_RECORD_BLOCKS", prop.multiProcessorCount * 8);
     c->geom.copy_blocks = env_int("HONU_COPY_BLOCKS", prop.multiProcessorCount * 4);
+    c->geom.copy_variant = env_int("HONU_COPY_VARIANT", 0);
     const uint64_t n = c->max_n;
     const uint64_t np = scan_partials_len(n, 3) + scan_partials_len(n, 1);
     const uint64_t bytes = 8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 256;
@@ -136,6 +137,15 @@ void honu_ctx_destroy(honu_ctx *ctx) {
 }
 
 uint64_t honu_ctx_max_records(const honu_ctx *ctx) { return ctx ? ctx->max_n : 0; }
+
+int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
+    if (!ctx || !name) return arg_fail("ctx/name");
+    if (!strcmp(name, "copy_blocks") && value > 0) ctx->geom.copy_blocks = (int)value;
+    else if (!strcmp(name, "record_blocks") && value > 0) ctx->geom.per_record_blocks = (int)value;
+    else if (!strcmp(name, "copy_variant") && value >= 0) ctx->geom.copy_variant = (int)value;
+    else return arg_fail(name);
+    return HONU_OK;
+}
 
 // ---------------------------------------------------------------------------
 // encode

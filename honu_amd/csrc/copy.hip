@@ -18,13 +18,6 @@
 
 namespace honu {
 
-#ifndef HONU_COPY_UNROLL
-#define HONU_COPY_UNROLL 4
-#endif
-#ifndef HONU_COPY_NT
-#define HONU_COPY_NT 0
-#endif
-
 // Segment i of an encode: src = payload[payload_off[i] ...], logical start =
 // payload_off[i], dst = out + out_off[i] + 1 + uvarint_len(len).
 struct EncodeSegments {
@@ -66,7 +59,7 @@ struct DecodeSegments {
     }
 };
 
-template <class Seg>
+template <class Seg, int UNROLL, bool NT>
 __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t n,
                                                                const uint64_t *__restrict__ total_p) {
     const uint64_t W = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
@@ -94,8 +87,24 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t 
         const uint64_t e = s + len;
         const uint64_t y = e < hi ? e : hi;
         if (x < y)
-            wave_copy<HONU_COPY_UNROLL, (bool)HONU_COPY_NT>(dst + (x - s), src + (x - s), y - x);
+            wave_copy<UNROLL, NT>(dst + (x - s), src + (x - s), y - x);
     }
+}
+
+// Copy-engine variants: {unroll depth, non-temporal loads/stores}. Variant 0
+// is the default; the others exist for the measurement sweeps in tools/.
+template <class Seg>
+static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
+                              const uint64_t *total, hipStream_t s) {
+    const dim3 grid(g.copy_blocks), block(HONU_BLOCK);
+    switch (g.copy_variant) {
+    case 1: hipLaunchKernelGGL((k_copy_segments<Seg, 8, false>), grid, block, 0, s, seg, n, total); break;
+    case 2: hipLaunchKernelGGL((k_copy_segments<Seg, 4, true>), grid, block, 0, s, seg, n, total); break;
+    case 3: hipLaunchKernelGGL((k_copy_segments<Seg, 8, true>), grid, block, 0, s, seg, n, total); break;
+    case 4: hipLaunchKernelGGL((k_copy_segments<Seg, 2, false>), grid, block, 0, s, seg, n, total); break;
+    default: hipLaunchKernelGGL((k_copy_segments<Seg, 4, false>), grid, block, 0, s, seg, n, total); break;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_encode_copy(const LaunchGeom &g, const uint8_t *payload,
@@ -103,9 +112,7 @@ hipError_t launch_encode_copy(const LaunchGeom &g, const uint8_t *payload,
                               const uint64_t *out_off, const int32_t *status, hipStream_t s) {
     if (n == 0) return hipSuccess;
     EncodeSegments seg{payload, payload_off, out, out_off, status};
-    hipLaunchKernelGGL(k_copy_segments<EncodeSegments>, dim3(g.copy_blocks), dim3(HONU_BLOCK), 0,
-                       s, seg, n, payload_off + n);
-    return hipGetLastError();
+    return launch_copy(g, seg, n, payload_off + n, s);
 }
 
 hipError_t launch_decode_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t n,
@@ -114,9 +121,7 @@ hipError_t launch_decode_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t 
                               hipStream_t s) {
     if (n == 0) return hipSuccess;
     DecodeSegments seg{rec, info, scratch, offs, data};
-    hipLaunchKernelGGL(k_copy_segments<DecodeSegments>, dim3(g.copy_blocks), dim3(HONU_BLOCK), 0,
-                       s, seg, n, totals + 2);
-    return hipGetLastError();
+    return launch_copy(g, seg, n, totals + 2, s);
 }
 
 }  // namespace honu

@@ -25,6 +25,7 @@ struct LaunchGeom {
     int num_cu;
     int per_record_blocks;  // cap on blocks for one-wave-per-record kernels
     int copy_blocks;        // blocks of the byte-balanced copy kernel
+    int copy_variant;       // copy engine variant (copy.hip: unroll depth / cache policy)
 };
 
 hipError_t launch_encode_sizes(const LaunchGeom &g, const honu_meta *meta, uint64_t var_len,

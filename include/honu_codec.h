@@ -185,6 +185,14 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err);
 void honu_ctx_destroy(honu_ctx *ctx);
 uint64_t honu_ctx_max_records(const honu_ctx *ctx);
 
+/* Launch-geometry knobs (defaults suit MI355X): "copy_blocks" (workgroups of
+ * the payload copy kernel, default 4 per CU), "record_blocks" (cap on
+ * workgroups of the one-wave-per-record kernels, default 8 per CU),
+ * "copy_variant" (copy-engine variant, default 0). Also settable at context
+ * creation through the environment (HONU_COPY_BLOCKS, HONU_RECORD_BLOCKS,
+ * HONU_COPY_VARIANT). */
+int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value);
+
 /* ABI self-description, used by bindings to check struct layouts. */
 uint32_t honu_abi_version(void);
 uint64_t honu_sizeof_meta(void);
