@@ -104,11 +104,13 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->max_n = max_records ? max_records : 1;
     c->geom.num_cu = prop.multiProcessorCount;
     c->geom.per_record_blocks = env_int("HONU_RECORD_BLOCKS", prop.multiProcessorCount * 8);
-    c->geom.copy_blocks = env_int("HONU_COPY_BLOCKS", prop.multiProcessorCount * 4);
+    c->geom.copy_blocks = env_int("HONU_COPY_BLOCKS", prop.multiProcessorCount * 2);
     c->geom.copy_variant = env_int("HONU_COPY_VARIANT", 0);
     const uint64_t n = c->max_n;
     const uint64_t np = scan_partials_len(n, 3) + scan_partials_len(n, 1);
-    const uint64_t bytes = 8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 256;
+    const uint64_t map_cap = 1ull << 22;  // tile map entries (sweep copy variants)
+    const uint64_t bytes =
+        8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 4 * map_cap + 256;
     if (hipMalloc(&c->ws, bytes) != hipSuccess) {
         snprintf(g_last_error, sizeof g_last_error, "hipMalloc(%llu) failed",
                  (unsigned long long)bytes);
@@ -126,6 +128,8 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->partials = w;
     w += np;
     c->scratch = (DecodeScratch *)w;
+    c->geom.tile_map = (uint32_t *)(c->scratch + n);
+    c->geom.tile_map_cap = map_cap;
     return c;
 }
 

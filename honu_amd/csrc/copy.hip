@@ -29,6 +29,10 @@ struct EncodeSegments {
 
     HONU_DEV uint64_t start(uint64_t i) const { return payload_off[i]; }
     HONU_DEV uint64_t lo() const { return payload_off[0]; }
+    HONU_DEV uint64_t end(uint64_t i, uint64_t total_abs) const {
+        (void)total_abs;
+        return payload_off[i + 1];
+    }
     HONU_DEV bool get(uint64_t i, uint64_t &len, const uint8_t *&src, uint8_t *&dst) const {
         if (status[i] != HONU_OK) return false;
         const uint64_t s = payload_off[i];
@@ -50,6 +54,8 @@ struct DecodeSegments {
 
     HONU_DEV uint64_t start(uint64_t i) const { return offs[3 * i + 2]; }
     HONU_DEV uint64_t lo() const { return 0; }
+    HONU_DEV uint64_t end(uint64_t i, uint64_t total_abs) const { return i + 1 < n_ ? offs[3 * i + 5] : total_abs; }
+    uint64_t n_;
     HONU_DEV bool get(uint64_t i, uint64_t &len, const uint8_t *&src, uint8_t *&dst) const {
         if (info[i].data_status != HONU_OK) return false;
         len = info[i].data_len;
@@ -91,17 +97,87 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t 
     }
 }
 
-// Copy-engine variants: {unroll depth, non-temporal loads/stores}. Variant 0
-// is the default; the others exist for the measurement sweeps in tools/.
+// ------------------------------------------------------------------------
+// Sweep form: the logical space is cut into tiles of T bytes and wave w
+// copies tiles w, w+W, w+2W, ... so that at any moment all waves work inside
+// one window of W*T bytes (DRAM rows opened by one wave are hit by its
+// neighbours) instead of W scattered streams. A prep kernel maps every tile to
+// the first segment overlapping it. T grows with the batch so the map fits
+// its fixed capacity.
+// ------------------------------------------------------------------------
+#define SWEEP_TILE_MIN (16u << 10)
+
+HONU_DEV uint64_t sweep_tile(uint64_t total, uint64_t map_cap) {
+    uint64_t t = (total + map_cap - 1) / map_cap;
+    t = (t + 4095) & ~4095ull;
+    return t < SWEEP_TILE_MIN ? SWEEP_TILE_MIN : t;
+}
+
+template <class Seg>
+__global__ __launch_bounds__(HONU_BLOCK) void k_tile_map(Seg seg, uint64_t n,
+                                                         const uint64_t *__restrict__ total_p,
+                                                         uint32_t *__restrict__ map, uint64_t map_cap) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t base = seg.lo();
+    const uint64_t total = *total_p - base;
+    const uint64_t T = sweep_tile(total, map_cap);
+    const uint64_t s = seg.start(i) - base, e = seg.end(i, *total_p) - base;
+    for (uint64_t t = (s + T - 1) / T; t * T < e; t++) map[t] = (uint32_t)i;
+}
+
+template <class Seg, int UNROLL>
+__global__ __launch_bounds__(HONU_BLOCK) void k_copy_sweep(Seg seg, uint64_t n,
+                                                            const uint64_t *__restrict__ total_p,
+                                                            const uint32_t *__restrict__ map,
+                                                            uint64_t map_cap) {
+    const uint64_t W = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
+    const uint64_t w = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + wave_in_block();
+    const uint64_t base = seg.lo();
+    const uint64_t total = *total_p - base;
+    const uint64_t T = sweep_tile(total, map_cap);
+    const uint64_t ntiles = (total + T - 1) / T;
+    for (uint64_t t = w; t < ntiles; t += W) {
+        const uint64_t lo = base + t * T;
+        const uint64_t hi = lo + T < base + total ? lo + T : base + total;
+        for (uint64_t i = map[t]; i < n; i++) {
+            const uint64_t s = seg.start(i);
+            if (s >= hi) break;
+            uint64_t len;
+            const uint8_t *src;
+            uint8_t *dst;
+            if (!seg.get(i, len, src, dst)) continue;
+            const uint64_t x = s > lo ? s : lo;
+            const uint64_t e = s + len;
+            const uint64_t y = e < hi ? e : hi;
+            if (x < y) wave_copy<UNROLL, false>(dst + (x - s), src + (x - s), y - x);
+        }
+    }
+}
+
+// Copy-engine variants: 0-5 contiguous per-wave ranges {unroll, non-temporal};
+// 6-7 the sweep form. Variant 0 is the default; the others exist for the
+// measurement sweeps in tools/tune_copy.py.
 template <class Seg>
 static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
                               const uint64_t *total, hipStream_t s) {
     const dim3 grid(g.copy_blocks), block(HONU_BLOCK);
+    if (g.copy_variant >= 6) {
+        if (!g.tile_map) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_tile_map<Seg>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                           seg, n, total, g.tile_map, g.tile_map_cap);
+        if (g.copy_variant == 7)
+            hipLaunchKernelGGL((k_copy_sweep<Seg, 8>), grid, block, 0, s, seg, n, total, g.tile_map, g.tile_map_cap);
+        else
+            hipLaunchKernelGGL((k_copy_sweep<Seg, 4>), grid, block, 0, s, seg, n, total, g.tile_map, g.tile_map_cap);
+        return hipGetLastError();
+    }
     switch (g.copy_variant) {
     case 1: hipLaunchKernelGGL((k_copy_segments<Seg, 8, false>), grid, block, 0, s, seg, n, total); break;
     case 2: hipLaunchKernelGGL((k_copy_segments<Seg, 4, true>), grid, block, 0, s, seg, n, total); break;
     case 3: hipLaunchKernelGGL((k_copy_segments<Seg, 8, true>), grid, block, 0, s, seg, n, total); break;
     case 4: hipLaunchKernelGGL((k_copy_segments<Seg, 2, false>), grid, block, 0, s, seg, n, total); break;
+    case 5: hipLaunchKernelGGL((k_copy_segments<Seg, 16, false>), grid, block, 0, s, seg, n, total); break;
     default: hipLaunchKernelGGL((k_copy_segments<Seg, 4, false>), grid, block, 0, s, seg, n, total); break;
     }
     return hipGetLastError();
@@ -120,7 +196,7 @@ hipError_t launch_decode_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t 
                               const uint64_t *offs, const uint64_t *totals, uint8_t *data,
                               hipStream_t s) {
     if (n == 0) return hipSuccess;
-    DecodeSegments seg{rec, info, scratch, offs, data};
+    DecodeSegments seg{rec, info, scratch, offs, data, n};
     return launch_copy(g, seg, n, totals + 2, s);
 }
 

@@ -26,6 +26,8 @@ struct LaunchGeom {
     int per_record_blocks;  // cap on blocks for one-wave-per-record kernels
     int copy_blocks;        // blocks of the byte-balanced copy kernel
     int copy_variant;       // copy engine variant (copy.hip: unroll depth / cache policy)
+    uint32_t *tile_map;     // sweep-form tile -> segment map (context scratch)
+    uint64_t tile_map_cap;
 };
 
 hipError_t launch_encode_sizes(const LaunchGeom &g, const honu_meta *meta, uint64_t var_len,

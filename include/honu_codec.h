@@ -186,7 +186,7 @@ void honu_ctx_destroy(honu_ctx *ctx);
 uint64_t honu_ctx_max_records(const honu_ctx *ctx);
 
 /* Launch-geometry knobs (defaults suit MI355X): "copy_blocks" (workgroups of
- * the payload copy kernel, default 4 per CU), "record_blocks" (cap on
+ * the payload copy kernel, default 2 per CU), "record_blocks" (cap on
  * workgroups of the one-wave-per-record kernels, default 8 per CU),
  * "copy_variant" (copy-engine variant, default 0). Also settable at context
  * creation through the environment (HONU_COPY_BLOCKS, HONU_RECORD_BLOCKS,

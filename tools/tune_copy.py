@@ -22,8 +22,8 @@ def main():
     ap.add_argument("--records", type=int, default=65536)
     ap.add_argument("--shape", default="large")
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--blocks", default="2,4,8,12,16")
-    ap.add_argument("--variants", default="0,1,2,3,4")
+    ap.add_argument("--blocks", default="1,2,4,8")
+    ap.add_argument("--variants", default="0,6,7")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     codec = Codec(0, a.records)
