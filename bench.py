@@ -52,11 +52,28 @@ def parse_args():
     p.add_argument("--cpu-records", type=int, default=2048)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--serial", action="store_true", help="one stream, no metadata/copy overlap")
+    p.add_argument("--meta-blocks", type=int, default=2,
+                   help="workgroups per CU for the per-record kernels (0 = library default)")
+    p.add_argument("--copy-prio", type=int, default=1, help="copy stream gets high priority")
     return p.parse_args()
 
 
 def P(t):
     return t.data_ptr()
+
+
+class Slot:
+    """Output buffers + codec context of one in-flight chunk."""
+
+    def __init__(self, dev, chunk, out_cap, acl_cap, reg_cap, data_cap):
+        E = lambda nb: torch.empty(int(nb), dtype=torch.uint8, device=dev)  # noqa: E731
+        self.codec = Codec(dev.index, max_records=chunk)
+        self.out_off, self.status = E(8 * (chunk + 1)), E(4 * chunk + 16)
+        self.out, self.dmeta, self.dinfo = E(out_cap), E(352 * chunk), E(32 * chunk)
+        self.dacl, self.dreg, self.data = E(20 * acl_cap), E(4 * reg_cap), E(data_cap)
+        self.totals = E(32)
+        self.free = None  # event: the slot's last copy finished
 
 
 class Bench:
@@ -85,17 +102,19 @@ class Bench:
         self.var_len, self.acl_len, self.reg_len = len(var), len(acl), len(reg)
         self.payload_bytes = int(off[N])
         self.payload = torch.empty(self.payload_bytes + 16, dtype=torch.uint8, device=self.dev)
+        s0 = torch.cuda.current_stream(self.dev).cuda_stream
         _lib.check(self.lib.honu_gen_payload(self.codec.ctx, args.seed, self.first, N, P(self.off),
-                                             P(self.payload), self.stream), "gen_payload")
+                                             P(self.payload), s0), "gen_payload")
         self.chunks = [(a, min(a + args.chunk, N)) for a in range(0, N, args.chunk)]
         C = args.chunk
-        self.out_off = torch.empty(8 * (C + 1), dtype=torch.uint8, device=self.dev)
-        self.status = torch.empty(4 * C + 16, dtype=torch.uint8, device=self.dev)
         # sizing pass (untimed): exact record bytes of every chunk
+        out_off = torch.empty(8 * (C + 1), dtype=torch.uint8, device=self.dev)
+        status = torch.empty(4 * C + 16, dtype=torch.uint8, device=self.dev)
         self.rec_bytes = []
         for a, b in self.chunks:
-            self._sizes(a, b)
-            self.rec_bytes.append(int(self.out_off.view(torch.int64)[b - a].item()))
+            self._sizes(self.codec, a, b, out_off, status, s0)
+            self.rec_bytes.append(int(out_off.view(torch.int64)[b - a].item()))
+        del out_off, status
         self.total_rec_bytes = sum(self.rec_bytes)
         lens = np.diff(off.astype(np.int64))
         acl_n = meta["acl_count"].astype(np.int64)
@@ -106,83 +125,109 @@ class Bench:
         self.reg_cap = max(int(reg_n[a:b].sum()) for a, b in self.chunks) + 1
         self.data_cap = max(int(alloc[a:b].sum()) for a, b in self.chunks) + 16
         self.out_cap = max(self.rec_bytes) + 16
-        self.out = torch.empty(self.out_cap, dtype=torch.uint8, device=self.dev)
-        self.dmeta = torch.empty(352 * C, dtype=torch.uint8, device=self.dev)
-        self.dinfo = torch.empty(32 * C, dtype=torch.uint8, device=self.dev)
-        self.dacl = torch.empty(20 * self.acl_cap, dtype=torch.uint8, device=self.dev)
-        self.dreg = torch.empty(4 * self.reg_cap, dtype=torch.uint8, device=self.dev)
-        self.data = torch.empty(self.data_cap, dtype=torch.uint8, device=self.dev)
-        self.totals = torch.empty(32, dtype=torch.uint8, device=self.dev)
+        nslots = 1 if args.serial else 2
+        self.slots = [Slot(self.dev, C, self.out_cap, self.acl_cap, self.reg_cap, self.data_cap)
+                      for _ in range(nslots)]
+        if args.meta_blocks:
+            ncu = torch.cuda.get_device_properties(self.dev).multi_processor_count
+            for sl in self.slots:
+                _lib.check(self.lib.honu_ctx_set_param(sl.codec.ctx, b"record_blocks",
+                                                       args.meta_blocks * ncu), "param")
+        self.sm = torch.cuda.Stream(self.dev)  # metadata kernels
+        # payload copies: the bandwidth-bound critical path, dispatched first
+        self.sc = (torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio else 0)
+                   if nslots == 2 else self.sm)
         self.events = None
+        self.last = None
         torch.cuda.synchronize()
 
-    @property
-    def stream(self):
-        return torch.cuda.current_stream(self.dev).cuda_stream
-
-    def _sizes(self, a, b):
+    def _sizes(self, codec, a, b, out_off, status, s):
         n = b - a
-        L, c, s = self.lib, self.codec.ctx, self.stream
+        L, c = self.lib, codec.ctx
         _lib.check(L.honu_encode_sizes(c, P(self.meta) + 352 * a, self.var_len, P(self.acl),
                                        self.acl_len, P(self.reg), self.reg_len, P(self.off) + 8 * a,
-                                       n, P(self.out_off), P(self.status), s), "sizes")
-        _lib.check(L.honu_exclusive_scan(c, P(self.out_off), n, P(self.out_off), s), "scan")
-
-    def _ev(self):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        return e
+                                       n, P(out_off), P(status), s), "sizes")
+        _lib.check(L.honu_exclusive_scan(c, P(out_off), n, P(out_off), s), "scan")
 
     def step(self, timed=False):
-        L, c = self.lib, self.codec.ctx
-        for a, b in self.chunks:
+        """Chunk k: metadata work (sizes, scan, headers+tails, parse, tables) on
+        stream sm, payload copies on stream sc; two slots so chunk k+1's metadata
+        work overlaps chunk k's copies. Only bytes outside the payloads are
+        touched by the metadata kernels, so they may run beside the copies."""
+        L = self.lib
+        sm, sc = self.sm, self.sc
+        for k, (a, b) in enumerate(self.chunks):
             n = b - a
-            s = self.stream
-            self._sizes(a, b)
+            sl = self.slots[k % len(self.slots)]
+            c = sl.codec.ctx
+            if sl.free is not None:
+                sm.wait_event(sl.free)
+            ms = sm.cuda_stream
+            self._sizes(sl.codec, a, b, sl.out_off, sl.status, ms)
             _lib.check(L.honu_encode_records(c, P(self.meta) + 352 * a, P(self.var), P(self.acl),
-                                             P(self.reg), P(self.off) + 8 * a, n, P(self.out),
-                                             self.out_cap, P(self.out_off), P(self.status), s),
+                                             P(self.reg), P(self.off) + 8 * a, n, P(sl.out),
+                                             self.out_cap, P(sl.out_off), P(sl.status), ms),
                        "encode_records")
-            e0 = self._ev() if timed else None
-            _lib.check(L.honu_encode_payloads(c, P(self.payload), P(self.off) + 8 * a, n,
-                                              P(self.out), P(self.out_off), P(self.status), s),
-                       "encode_payloads")
-            e1 = self._ev() if timed else None
-            _lib.check(L.honu_decode_parse(c, P(self.out), P(self.out_off), n, P(self.dmeta),
-                                           P(self.dinfo), s), "decode_parse")
-            _lib.check(L.honu_decode_tables(c, P(self.out), n, P(self.dmeta), P(self.dinfo),
-                                            P(self.dacl), self.acl_cap, P(self.dreg), self.reg_cap,
-                                            P(self.data), self.data_cap, P(self.totals), s),
+            ev_meta = torch.cuda.Event()
+            ev_meta.record(sm)
+            _lib.check(L.honu_decode_parse(c, P(sl.out), P(sl.out_off), n, P(sl.dmeta),
+                                           P(sl.dinfo), ms), "decode_parse")
+            _lib.check(L.honu_decode_tables(c, P(sl.out), n, P(sl.dmeta), P(sl.dinfo),
+                                            P(sl.dacl), self.acl_cap, P(sl.dreg), self.reg_cap,
+                                            P(sl.data), self.data_cap, P(sl.totals), ms),
                        "decode_tables")
-            e2 = self._ev() if timed else None
-            _lib.check(L.honu_decode_payloads(c, P(self.out), n, P(self.dinfo), P(self.data),
-                                              P(self.totals), s), "decode_payloads")
-            e3 = self._ev() if timed else None
+            ev_fill = torch.cuda.Event()
+            ev_fill.record(sm)
+            cs = sc.cuda_stream
+            sc.wait_event(ev_meta)
+            e0 = torch.cuda.Event(enable_timing=True) if timed else None
+            e1 = torch.cuda.Event(enable_timing=True) if timed else None
             if timed:
+                e0.record(sc)
+            _lib.check(L.honu_encode_payloads(c, P(self.payload), P(self.off) + 8 * a, n,
+                                              P(sl.out), P(sl.out_off), P(sl.status), cs),
+                       "encode_payloads")
+            if timed:
+                e1.record(sc)
+            sc.wait_event(ev_fill)
+            e2 = torch.cuda.Event(enable_timing=True) if timed else None
+            e3 = torch.cuda.Event(enable_timing=True) if timed else None
+            if timed:
+                e2.record(sc)
+            _lib.check(L.honu_decode_payloads(c, P(sl.out), n, P(sl.dinfo), P(sl.data),
+                                              P(sl.totals), cs), "decode_payloads")
+            if timed:
+                e3.record(sc)
                 self.events.append((a, b, e0, e1, e2, e3))
+            sl.free = torch.cuda.Event()
+            sl.free.record(sc)
+            self.last = (a, b, sl)
+        torch.cuda.current_stream(self.dev).wait_stream(sc)
+        torch.cuda.current_stream(self.dev).wait_stream(sm)
 
     def verify(self):
         """Size-independent checks on the last chunk of the last step: every
         status is OK, every decoded payload digest equals its source digest,
-        and sampled decoded rows equal the input rows."""
-        L, c, s = self.lib, self.codec.ctx, self.stream
-        a, b = self.chunks[-1]
+        and the decoded rows equal the input rows."""
+        torch.cuda.synchronize()
+        a, b, sl = self.last
+        L, c, s = self.lib, sl.codec.ctx, torch.cuda.current_stream(self.dev).cuda_stream
         n = b - a
-        st = self.status[: 4 * n].view(torch.int32)
-        info = self.dinfo[: 32 * n].view(torch.int64).view(n, 4)
+        st = sl.status[: 4 * n].view(torch.int32)
+        info = sl.dinfo[: 32 * n].view(torch.int64).view(n, 4)
         ms = info[:, 2].contiguous().view(torch.int32)
         dsrc = torch.empty(8 * n, dtype=torch.uint8, device=self.dev)
         ddst = torch.empty(8 * n, dtype=torch.uint8, device=self.dev)
         _lib.check(L.honu_digest_records(c, P(self.payload), P(self.off) + 8 * a, 0, n, P(dsrc), s),
                    "digest")
         doff, dlen = info[:, 0].contiguous(), info[:, 1].contiguous()
-        _lib.check(L.honu_digest_records(c, P(self.data), P(doff), P(dlen), n, P(ddst), s), "digest")
+        _lib.check(L.honu_digest_records(c, P(sl.data), P(doff), P(dlen), n, P(ddst), s), "digest")
         torch.cuda.synchronize()
         ok = bool((st == 0).all()) and bool((ms == 0).all())
         ok &= torch.equal(dsrc, ddst)
         exp_len = torch.from_numpy(np.diff(self.host_off[a:b + 1].astype(np.int64))).to(self.dev)
         ok &= torch.equal(dlen, exp_len)
-        rows = self.dmeta[: 352 * n].cpu().numpy().view(self.host_meta.dtype)
+        rows = sl.dmeta[: 352 * n].cpu().numpy().view(self.host_meta.dtype)
         src = self.host_meta[a:b]
         for f in ("present", "pid", "vid", "region", "created", "modified", "acl_count",
                   "regions_count", "permissions", "flags", "owner", "group"):
@@ -333,6 +378,8 @@ def main():
             "encoded_bytes_per_gpu": bench.total_rec_bytes,
             "payload_bytes_per_gpu": bench.payload_bytes,
             "parallelism": f"dp{world} (records sharded, no data-path collective)",
+            "streams": 1 if args.serial else 2,
+            "meta_blocks_per_cu": args.meta_blocks or 8,
         },
         "records_per_s": total_records / step_s,
         "roofline": {
