@@ -128,7 +128,7 @@ class Bench:
         nslots = 1 if args.serial else 2
         self.slots = [Slot(self.dev, C, self.out_cap, self.acl_cap, self.reg_cap, self.data_cap)
                       for _ in range(nslots)]
-        if args.meta_blocks:
+        if args.meta_blocks and not args.serial:
             ncu = torch.cuda.get_device_properties(self.dev).multi_processor_count
             for sl in self.slots:
                 _lib.check(self.lib.honu_ctx_set_param(sl.codec.ctx, b"record_blocks",
@@ -379,7 +379,7 @@ def main():
             "payload_bytes_per_gpu": bench.payload_bytes,
             "parallelism": f"dp{world} (records sharded, no data-path collective)",
             "streams": 1 if args.serial else 2,
-            "meta_blocks_per_cu": args.meta_blocks or 8,
+            "meta_blocks_per_cu": 8 if (args.serial or not args.meta_blocks) else args.meta_blocks,
         },
         "records_per_s": total_records / step_s,
         "roofline": {
