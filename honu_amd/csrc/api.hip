@@ -106,6 +106,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->geom.per_record_blocks = env_int("HONU_RECORD_BLOCKS", prop.multiProcessorCount * 8);
     c->geom.copy_blocks = env_int("HONU_COPY_BLOCKS", prop.multiProcessorCount * 2);
     c->geom.copy_variant = env_int("HONU_COPY_VARIANT", 0);
+    c->geom.record_variant = env_int("HONU_RECORD_VARIANT", 0);
     const uint64_t n = c->max_n;
     const uint64_t np = scan_partials_len(n, 3) + scan_partials_len(n, 1);
     const uint64_t map_cap = 1ull << 22;  // tile map entries (sweep copy variants)
@@ -147,6 +148,7 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
     if (!strcmp(name, "copy_blocks") && value > 0) ctx->geom.copy_blocks = (int)value;
     else if (!strcmp(name, "record_blocks") && value > 0) ctx->geom.per_record_blocks = (int)value;
     else if (!strcmp(name, "copy_variant") && value >= 0) ctx->geom.copy_variant = (int)value;
+    else if (!strcmp(name, "record_variant") && value >= 0) ctx->geom.record_variant = (int)value;
     else return arg_fail(name);
     return HONU_OK;
 }
@@ -162,8 +164,13 @@ int32_t honu_encode_sizes(honu_ctx *ctx, const honu_meta *d_meta, uint64_t var_l
     if (n && (!d_meta || !d_payload_off || !d_sizes)) return arg_fail("null pointer");
     if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(launch_encode_sizes(ctx->geom, d_meta, var_len, d_acl, acl_len, d_regions, regions_len,
-                               d_payload_off, n, d_sizes, d_status, (hipStream_t)stream));
+    if (ctx->geom.record_variant == 0)
+        HIPCHK(launch_encode_sizes_lane(d_meta, var_len, d_acl, acl_len, d_regions, regions_len,
+                                        d_payload_off, n, d_sizes, d_status, (hipStream_t)stream));
+    else
+        HIPCHK(launch_encode_sizes(ctx->geom, d_meta, var_len, d_acl, acl_len, d_regions,
+                                   regions_len, d_payload_off, n, d_sizes, d_status,
+                                   (hipStream_t)stream));
     return HONU_OK;
 }
 
@@ -243,8 +250,12 @@ int32_t honu_decode_parse(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
     if (!aligned(d_rec, 16) || !aligned(d_meta, 16) || !aligned(d_info, 8))
         return arg_fail("records arena and rows must be 16-byte aligned");
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(launch_decode_parse(ctx->geom, d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
-                               ctx->counts, (hipStream_t)stream));
+    if (ctx->geom.record_variant == 0)
+        HIPCHK(launch_decode_parse_lane(d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
+                                        ctx->counts, (hipStream_t)stream));
+    else
+        HIPCHK(launch_decode_parse(ctx->geom, d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
+                                   ctx->counts, (hipStream_t)stream));
     return HONU_OK;
 }
 
@@ -262,9 +273,14 @@ int32_t honu_decode_tables(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n, honu
     hipStream_t s = (hipStream_t)stream;
     uint64_t *tot = d_totals ? d_totals : ctx->totals;
     HIPCHK(launch_scan(ctx->counts, n, 3, ctx->offs, tot, ctx->partials, s));
-    HIPCHK(launch_decode_fill(ctx->geom, d_rec, n, d_meta, d_info, ctx->scratch, ctx->counts,
-                              ctx->offs, tot, d_acl, acl_cap, d_regions, regions_cap, d_data,
-                              data_cap, s));
+    if (ctx->geom.record_variant == 0)
+        HIPCHK(launch_decode_fill_lane(d_rec, n, d_meta, d_info, ctx->scratch, ctx->counts,
+                                       ctx->offs, d_acl, acl_cap, d_regions, regions_cap, d_data,
+                                       data_cap, s));
+    else
+        HIPCHK(launch_decode_fill(ctx->geom, d_rec, n, d_meta, d_info, ctx->scratch, ctx->counts,
+                                  ctx->offs, tot, d_acl, acl_cap, d_regions, regions_cap, d_data,
+                                  data_cap, s));
     return HONU_OK;
 }
 

@@ -26,6 +26,7 @@ struct LaunchGeom {
     int per_record_blocks;  // cap on blocks for one-wave-per-record kernels
     int copy_blocks;        // blocks of the byte-balanced copy kernel
     int copy_variant;       // copy engine variant (copy.hip: unroll depth / cache policy)
+    int record_variant;     // 0: one record per lane (lane.hip), 1: one record per wave
     uint32_t *tile_map;     // sweep-form tile -> segment map (context scratch)
     uint64_t tile_map_cap;
 };
@@ -59,6 +60,19 @@ hipError_t launch_decode_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t 
 hipError_t launch_decode_keys(const LaunchGeom &g, const honu_meta *meta,
                               const honu_record_info *info, uint64_t n, uint8_t *keys,
                               int32_t *key_status, hipStream_t s);
+
+hipError_t launch_decode_parse_lane(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                                    honu_meta *meta, honu_record_info *info,
+                                    DecodeScratch *scratch, uint64_t *counts, hipStream_t s);
+hipError_t launch_decode_fill_lane(const uint8_t *rec, uint64_t n, honu_meta *meta,
+                                   honu_record_info *info, const DecodeScratch *scratch,
+                                   const uint64_t *counts, const uint64_t *offs, honu_acl *acl,
+                                   uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap,
+                                   uint8_t *data, uint64_t data_cap, hipStream_t s);
+hipError_t launch_encode_sizes_lane(const honu_meta *meta, uint64_t var_len, const honu_acl *acl,
+                                    uint64_t acl_len, const uint32_t *reg, uint64_t reg_len,
+                                    const uint64_t *payload_off, uint64_t n, uint64_t *sizes,
+                                    int32_t *status, hipStream_t s);
 
 // Exclusive scan of K interleaved u64 columns: out[i*K+c] = sum_{j<i} in[j*K+c];
 // totals[c] = full sum. `partials` needs scan_partials_len(n, K) u64.

@@ -1,0 +1,173 @@
+// lane.h — per-lane lani cursor: one record per LANE.
+//
+// The Metadata grammar is a serial walk (every field's position depends on
+// the previous varint), so a wave that walks one record with 64 lanes in
+// lockstep issues the whole walk 64 times over for one record's worth of
+// work: measured ~1 ms per 65,536 records, VALU-issue bound. Here each lane
+// walks its own record: 64 records per wave-instruction stream.
+//
+// Bytes come from 16-byte windows: the two aligned 16-byte blocks around the
+// cursor, funnel-shifted by the lane's own byte phase. Successive fields of a
+// record sit in the same few cache lines, so after the first touch the
+// window loads hit L1/L2. Varints are decoded branch-free from the window:
+// the terminator is the first byte with a clear top bit (bit mask + ctz) and
+// the 7-bit groups are compacted in three shift/mask steps.
+#pragma once
+
+#include "common.h"
+
+namespace honu {
+
+// Bytes [q, q+16) of the arena as two little-endian u64 (bytes at or beyond
+// `end` are unspecified). Requires q < end. The second aligned block is read
+// only when it holds a byte below `end`, so no load leaves mapped memory.
+HONU_DEV void lane_fetch16(const uint8_t *__restrict__ base, uint64_t q, uint64_t end,
+                           uint64_t &lo, uint64_t &hi) {
+    const uint64_t A = q & ~15ull;
+    const uint32_t s = (uint32_t)(q & 15);
+    const u32x4 a = *reinterpret_cast<const u32x4 *>(base + A);
+    u32x4 b = {0, 0, 0, 0};
+    if (s && A + 16 < end) b = *reinterpret_cast<const u32x4 *>(base + A + 16);
+    const uint32_t q4 = s >> 2, sh = s & 3;
+    // w[k] = word k of a||b; pick(j) = w[q4 + j] for j in 0..4 (per-lane q4)
+    const uint32_t w0 = a.x, w1 = a.y, w2 = a.z, w3 = a.w, w4 = b.x, w5 = b.y, w6 = b.z, w7 = b.w;
+    const bool o1 = q4 & 1, o2 = q4 & 2;
+#define PICK(j0, j1, j2, j3) (o2 ? (o1 ? (j3) : (j2)) : (o1 ? (j1) : (j0)))
+    const uint32_t p0 = PICK(w0, w1, w2, w3);
+    const uint32_t p1 = PICK(w1, w2, w3, w4);
+    const uint32_t p2 = PICK(w2, w3, w4, w5);
+    const uint32_t p3 = PICK(w3, w4, w5, w6);
+    const uint32_t p4 = PICK(w4, w5, w6, w7);
+#undef PICK
+    const uint32_t r0 = __builtin_amdgcn_alignbyte(p1, p0, sh);
+    const uint32_t r1 = __builtin_amdgcn_alignbyte(p2, p1, sh);
+    const uint32_t r2 = __builtin_amdgcn_alignbyte(p3, p2, sh);
+    const uint32_t r3 = __builtin_amdgcn_alignbyte(p4, p3, sh);
+    lo = ((uint64_t)r1 << 32) | r0;
+    hi = ((uint64_t)r3 << 32) | r2;
+}
+
+// Compact the 7-bit groups of up to 8 varint bytes (top bits already clear).
+HONU_DEV uint64_t compact7(uint64_t x) {
+    x = (x & 0x007F007F007F007Full) | ((x & 0x7F007F007F007F00ull) >> 1);
+    x = (x & 0x00003FFF00003FFFull) | ((x & 0x3FFF00003FFF0000ull) >> 2);
+    x = (x & 0x000000000FFFFFFFull) | ((x & 0x0FFFFFFF00000000ull) >> 4);
+    return x;
+}
+
+// binary.Uvarint over the first n (1..10) bytes of the window lo||hi.
+// Returns k > 0 (bytes consumed) or 0 when Go's Uvarint returns k <= 0
+// (no terminator inside the window, or 64-bit overflow at the 10th byte).
+HONU_DEV uint32_t uvarint_window(uint64_t lo, uint64_t hi, uint32_t n, uint64_t &v) {
+    const uint64_t tl = ~lo & 0x8080808080808080ull;
+    const uint64_t th = ~hi & 0x0000000000008080ull;
+    uint32_t k;
+    if (tl) k = (uint32_t)(__builtin_ctzll(tl) >> 3) + 1;
+    else if (th) k = (uint32_t)(__builtin_ctzll(th) >> 3) + 9;
+    else k = 11;
+    if (k > n) return 0;
+    if (k == 10 && ((hi >> 8) & 0xFF) > 1) return 0;  // overflow (varint.go)
+    const uint64_t m = k >= 8 ? lo : (lo & ((1ull << (8 * k)) - 1));
+    uint64_t x = compact7(m & 0x7F7F7F7F7F7F7F7Full);
+    if (k >= 9) x |= (hi & 0x7F) << 56;
+    if (k == 10) x |= ((hi >> 8) & 0x7F) << 63;
+    v = x;
+    return k;
+}
+
+// Row image in registers: 88 dwords of honu_meta, indices static.
+struct Row {
+    uint32_t d[88];
+    HONU_DEV void clear() {
+#pragma unroll
+        for (int i = 0; i < 88; i++) d[i] = 0;
+    }
+    HONU_DEV void u8(int off, uint32_t v) { d[off >> 2] |= (v & 0xFF) << (8 * (off & 3)); }
+    HONU_DEV void u32(int off, uint32_t v) { d[off >> 2] = v; }
+    HONU_DEV void u64(int off, uint64_t v) {
+        d[off >> 2] = (uint32_t)v;
+        d[(off >> 2) + 1] = (uint32_t)(v >> 32);
+    }
+    HONU_DEV void bytes16(int off, uint64_t lo, uint64_t hi) {
+        u64(off, lo);
+        u64(off + 8, hi);
+    }
+    HONU_DEV void span(int off, uint64_t o, uint64_t l) {
+        u64(off, o);
+        u64(off + 8, l);
+    }
+    HONU_DEV void store(honu_meta *dst) const {
+        u32x4 *p = reinterpret_cast<u32x4 *>(dst);
+#pragma unroll
+        for (int i = 0; i < 22; i++) p[i] = u32x4{d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]};
+    }
+};
+
+// lani.Decoder (lani/decode.go) over [tstart, end) for one lane.
+struct LaneDec {
+    const uint8_t *base;
+    uint64_t p, end, tstart;
+
+    HONU_DEV int u8(uint32_t &v) {  // DecodeByte :94-103
+        if (p >= end) return HONU_ERR_EOF;
+        v = base[p];
+        p += 1;
+        return HONU_OK;
+    }
+    HONU_DEV int boolean(uint32_t &v) {  // DecodeBool :105-120
+        int st = u8(v);
+        if (st) return st;
+        return v > 1 ? HONU_ERR_PARSE_BOOLEAN : HONU_OK;
+    }
+    HONU_DEV int uv(uint32_t maxw, int err, uint64_t &v) {
+        if (p >= end) return HONU_ERR_EOF;
+        const uint64_t avail = end - p;
+        const uint32_t n = avail < maxw ? (uint32_t)avail : maxw;
+        uint64_t lo, hi;
+        lane_fetch16(base, p, end, lo, hi);
+        const uint32_t k = uvarint_window(lo, hi, n, v);
+        if (!k) return err;
+        p += k;
+        return HONU_OK;
+    }
+    HONU_DEV int u32(uint32_t &v) {  // DecodeUint32 :127-146
+        uint64_t x = 0;
+        int st = uv(5, HONU_ERR_PARSE_VARINT, x);
+        v = (uint32_t)x;
+        return st;
+    }
+    HONU_DEV int u64(uint64_t &v) { return uv(10, HONU_ERR_PARSE_VARINT, v); }  // :149-168
+    HONU_DEV int i64(int64_t &v) {                                             // :171-190
+        uint64_t x = 0;
+        int st = uv(10, HONU_ERR_PARSE_VARINT, x);
+        v = unzigzag(x);
+        return st;
+    }
+    HONU_DEV int ulid(uint64_t &lo, uint64_t &hi) {  // DecodeULID :209-221
+        if (p >= end) return HONU_ERR_EOF;
+        if (p + 16 > end) return HONU_ERR_UNEXPECTED_EOF;
+        lane_fetch16(base, p, end, lo, hi);
+        p += 16;
+        return HONU_OK;
+    }
+    // Decode :30-56 with readLength :261-282 -> zero-copy span.
+    HONU_DEV int frame(uint64_t &off, uint64_t &len) {
+        uint64_t rl = 0;
+        int st = uv(10, HONU_ERR_NO_LENGTH, rl);
+        if (st) return st;
+        if (rl >= (1ull << 63)) return HONU_ERR_PANIC;  // int(rl) < 0 -> makeslice
+        if (rl == 0) {
+            off = 0;
+            len = 0;
+            return HONU_OK;
+        }
+        if (rl > (uint64_t)INT64_MAX - (p - tstart)) return HONU_ERR_PANIC;  // d.i + rl overflows
+        if (p + rl > end) return HONU_ERR_UNEXPECTED_EOF;
+        off = p;
+        len = rl;
+        p += rl;
+        return HONU_OK;
+    }
+};
+
+}  // namespace honu

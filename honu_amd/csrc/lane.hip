@@ -1,0 +1,350 @@
+// lane.hip — the per-record metadata kernels with one record per LANE
+// (see lane.h for why): decode parse, decode fill and the encode size pass.
+#include "kernels.h"
+#include "lane.h"
+
+namespace honu {
+
+#define GO_MAX_ALLOC (1ull << 48)  // runtime maxAlloc, linux/amd64
+#define OFF(f) ((int)offsetof(honu_meta, f))
+
+#define TRY(x)              \
+    do {                    \
+        st = (x);           \
+        if (st) goto done;  \
+    } while (0)
+
+// ------------------------------------------------------------------------
+// decode parse: Object.Metadata() + Data() + Tombstone() + StorageVersion()
+// (object.go:47-134) with the lani walk of metadata.go:202-302.
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_lane(
+    const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
+    honu_meta *__restrict__ meta, honu_record_info *__restrict__ info,
+    DecodeScratch *__restrict__ scratch, uint64_t *__restrict__ counts) {
+    const uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t beg = rec_off[i], end = rec_off[i + 1];
+    const uint64_t len = end - beg;
+    uint32_t ver = 0;
+    int64_t d = -1, b = -1;
+    if (len) {
+        uint64_t lo, hi;
+        lane_fetch16(rec, beg, end, lo, hi);
+        ver = (uint32_t)(lo & 0xFF);
+        // dataLength (object.go:114-134): Uvarint(o[1 : min(11, len-1)])
+        if (len >= 3) {
+            const uint32_t wl = (uint32_t)(len - 2 < 10 ? len - 2 : 10);
+            const uint64_t lo1 = (lo >> 8) | (hi << 56), hi1 = hi >> 8;
+            uint64_t x;
+            const uint32_t k = uvarint_window(lo1, hi1, wl, x);
+            if (k) {
+                d = (int64_t)x;  // int(rl): negative for rl >= 2^63
+                b = k;
+            }
+        }
+    }
+    const bool v1 = ver == HONU_STORAGE_VERSION;
+    const bool in_range = d >= 0 && (uint64_t)d <= len - 1 - (uint64_t)b;
+    int32_t data_status;
+    uint64_t data_off = 0, data_len = 0;
+    if (!v1) data_status = HONU_ERR_BAD_VERSION;
+    else if (d < 0) data_status = HONU_ERR_MALFORMED;
+    else if (d == 0) data_status = HONU_OK;
+    else if (!in_range) data_status = HONU_ERR_PANIC;  // o[1+b:1+b+d]
+    else {
+        data_status = HONU_OK;
+        data_off = beg + 1 + (uint64_t)b;
+        data_len = (uint64_t)d;
+    }
+
+    Row R;
+    R.clear();
+    uint64_t nacl = 0, nreg = 0, acl_pos = 0, reg_pos = 0;
+    int st = HONU_OK;
+    if (!v1) st = HONU_ERR_BAD_VERSION;
+    else if (d < 0) st = HONU_ERR_MALFORMED;
+    else if (!in_range) st = HONU_ERR_PANIC;  // o[1+d+b:]
+    else {
+        LaneDec D;
+        D.base = rec;
+        D.end = end;
+        D.tstart = beg + 1 + (uint64_t)b + (uint64_t)d;
+        D.p = D.tstart;
+        uint32_t f, u;
+        uint64_t v, o, l, lo, hi;
+        int64_t t;
+        uint32_t pr = 0;
+        TRY(D.boolean(f));                                      // DecodeStruct(meta) object.go:78
+        if (f) {
+            pr = HONU_HAS_META;
+            TRY(D.ulid(lo, hi)); R.bytes16(OFF(object_id), lo, hi);        // metadata.go:210
+            TRY(D.ulid(lo, hi)); R.bytes16(OFF(collection_id), lo, hi);    // :214
+            TRY(D.boolean(f));                                  // :219 Version
+            if (f) {
+                pr |= HONU_HAS_VERSION;
+                TRY(D.u32(u)); R.u32(OFF(pid), u);              // scalar.go:121-131
+                TRY(D.u64(v)); R.u64(OFF(vid), v);
+                TRY(D.u32(u)); R.u32(OFF(region), u);           // version.go:80
+                TRY(D.boolean(f));                              // :88 Parent
+                if (f) {
+                    pr |= HONU_HAS_PARENT;
+                    TRY(D.u32(u)); R.u32(OFF(parent_pid), u);
+                    TRY(D.u64(v)); R.u64(OFF(parent_vid), v);
+                }
+                TRY(D.boolean(f)); R.u8(OFF(tombstone), f);     // :96
+                TRY(D.i64(t)); R.u64(OFF(version_created), (uint64_t)t);  // :100
+            }
+            TRY(D.boolean(f));                                  // :225 Schema
+            if (f) {
+                pr |= HONU_HAS_SCHEMA;
+                TRY(D.frame(o, l)); R.span(OFF(schema_name), o, l);        // schema.go:55-73
+                TRY(D.u32(u)); R.u32(OFF(schema_major), u);
+                TRY(D.u32(u)); R.u32(OFF(schema_minor), u);
+                TRY(D.u32(u)); R.u32(OFF(schema_patch), u);
+            }
+            TRY(D.frame(o, l)); R.span(OFF(mime), o, l);        // :231
+            TRY(D.ulid(lo, hi)); R.bytes16(OFF(owner), lo, hi); // :235
+            TRY(D.ulid(lo, hi)); R.bytes16(OFF(group), lo, hi); // :239
+            TRY(D.u8(u)); R.u8(OFF(permissions), u);            // :243
+            TRY(D.u64(nacl));                                   // :249
+            if (nacl > 0) {                                     // :254-265
+                if (nacl > GO_MAX_ALLOC / 8) TRY(HONU_ERR_PANIC);  // make([]*AccessControl)
+                acl_pos = D.p;
+                for (uint64_t k = 0; k < nacl; k++) {           // acls.go:41-51
+                    TRY(D.boolean(f));
+                    if (f) {
+                        if (D.p >= D.end) TRY(HONU_ERR_EOF);
+                        if (D.p + 16 > D.end) TRY(HONU_ERR_UNEXPECTED_EOF);
+                        D.p += 16;
+                        TRY(D.u8(u));
+                    }
+                }
+                R.u64(OFF(acl_count), nacl);
+            }
+            TRY(D.u64(nreg));                                   // region.go:154-169
+            if (nreg > GO_MAX_ALLOC / 4) TRY(HONU_ERR_PANIC);   // make(Regions, length)
+            pr |= HONU_REGIONS_NONNIL;
+            reg_pos = D.p;
+            for (uint64_t k = 0; k < nreg; k++) TRY(D.u32(u));
+            R.u64(OFF(regions_count), nreg);
+            TRY(D.boolean(f));                                  // :271 Publisher
+            if (f) {
+                pr |= HONU_HAS_PUBLISHER;
+                TRY(D.ulid(lo, hi)); R.bytes16(OFF(publisher_id), lo, hi);  // provenance.go:59-79
+                TRY(D.ulid(lo, hi)); R.bytes16(OFF(client_id), lo, hi);
+                TRY(D.frame(o, l)); R.span(OFF(ip_address), o, l);
+                TRY(D.frame(o, l)); R.span(OFF(user_agent), o, l);
+            }
+            TRY(D.boolean(f));                                  // :277 Encryption
+            if (f) {
+                pr |= HONU_HAS_ENCRYPTION;
+                TRY(D.frame(o, l)); R.span(OFF(public_key_id), o, l);      // encryption.go:91-125
+                TRY(D.frame(o, l)); R.span(OFF(encryption_key), o, l);
+                TRY(D.frame(o, l)); R.span(OFF(hmac_secret), o, l);
+                TRY(D.frame(o, l)); R.span(OFF(signature), o, l);
+                TRY(D.u8(u)); R.u8(OFF(sealing_alg), u);
+                TRY(D.u8(u)); R.u8(OFF(encryption_alg), u);
+                TRY(D.u8(u)); R.u8(OFF(signature_alg), u);
+            }
+            TRY(D.boolean(f));                                  // :283 Compression
+            if (f) {
+                pr |= HONU_HAS_COMPRESSION;
+                TRY(D.u8(u)); R.u8(OFF(compression_alg), u);    // compression.go:55-67
+                TRY(D.i64(t)); R.u64(OFF(compression_level), (uint64_t)t);
+            }
+            TRY(D.u8(u)); R.u8(OFF(flags), u);                  // :289
+            TRY(D.i64(t)); R.u64(OFF(created), (uint64_t)t);    // :293
+            TRY(D.i64(t)); R.u64(OFF(modified), (uint64_t)t);   // :297
+        }
+        R.u32(OFF(present), pr);
+    }
+done:
+    if (st != HONU_OK) {  // Go returns nil, err
+        R.clear();
+        nacl = nreg = 0;
+    }
+    R.store(meta + i);
+    honu_record_info inf;
+    inf.data_off = data_off;
+    inf.data_len = data_len;
+    inf.data_status = data_status;
+    inf.meta_status = st;
+    inf.storage_version = (uint8_t)ver;
+    inf.tombstone = (v1 && d == 0) ? 1 : 0;  // Tombstone :103-112
+#pragma unroll
+    for (int k = 0; k < 6; k++) inf._pad[k] = 0;
+    info[i] = inf;
+    scratch[i] = DecodeScratch{acl_pos, reg_pos, data_off, end};
+    counts[3 * i + 0] = nacl;
+    counts[3 * i + 1] = nreg;
+    counts[3 * i + 2] = (data_len + 15) & ~15ull;
+}
+
+// ------------------------------------------------------------------------
+// decode fill: ACL/region tables and offsets (after the count scans)
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_lane(
+    const uint8_t *__restrict__ rec, uint64_t n, honu_meta *__restrict__ meta,
+    honu_record_info *__restrict__ info, const DecodeScratch *__restrict__ scratch,
+    const uint64_t *__restrict__ counts, const uint64_t *__restrict__ offs,
+    honu_acl *__restrict__ acl, uint64_t acl_cap, uint32_t *__restrict__ reg, uint64_t reg_cap,
+    uint8_t *__restrict__ data, uint64_t data_cap) {
+    const uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    honu_record_info *inf = info + i;
+    if (inf->meta_status == HONU_OK) {
+        const uint64_t na = counts[3 * i], nr = counts[3 * i + 1];
+        const uint64_t ao = offs[3 * i], ro = offs[3 * i + 1];
+        if (na) meta[i].acl_off = ao;
+        if (nr) meta[i].regions_off = ro;
+        if (ao + na > acl_cap || ro + nr > reg_cap) {
+            inf->meta_status = HONU_ERR_CAPACITY;
+        } else if (na + nr) {
+            const DecodeScratch sc = scratch[i];
+            const uint64_t end = sc.rec_end;
+            uint64_t p = sc.acl_pos;
+            for (uint64_t k = 0; k < na; k++) {  // validated by the parse
+                uint32_t *e = reinterpret_cast<uint32_t *>(acl + ao + k);
+                if (rec[p]) {
+                    uint64_t lo, hi;
+                    lane_fetch16(rec, p + 1, end, lo, hi);
+                    e[0] = (uint32_t)lo;
+                    e[1] = (uint32_t)(lo >> 32);
+                    e[2] = (uint32_t)hi;
+                    e[3] = (uint32_t)(hi >> 32);
+                    e[4] = (uint32_t)rec[p + 17] | (1u << 8);
+                    p += 18;
+                } else {
+                    e[0] = e[1] = e[2] = e[3] = e[4] = 0;
+                    p += 1;
+                }
+            }
+            p = sc.regions_pos;
+            for (uint64_t k = 0; k < nr; k++) {
+                const uint64_t avail = end - p;
+                uint64_t lo, hi, v = 0;
+                lane_fetch16(rec, p, end, lo, hi);
+                const uint32_t kk = uvarint_window(lo, hi, avail < 5 ? (uint32_t)avail : 5, v);
+                reg[ro + k] = (uint32_t)v;
+                p += kk;
+            }
+        }
+    }
+    if (data && inf->data_status == HONU_OK && inf->data_len) {
+        const uint64_t doff = offs[3 * i + 2];
+        if (doff + inf->data_len > data_cap) {
+            inf->data_status = HONU_ERR_CAPACITY;
+            inf->data_off = 0;
+            inf->data_len = 0;
+        } else {
+            inf->data_off = doff;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
+// encode size pass: exact record length (object.go:24-45 / App. A)
+// ------------------------------------------------------------------------
+HONU_DEV bool span_in(uint64_t off, uint64_t len, uint64_t var_len) {
+    return len == 0 || (off <= var_len && len <= var_len - off);
+}
+HONU_DEV uint64_t frame_len(uint64_t len) { return uvarint_len(len) + len; }
+
+__global__ __launch_bounds__(HONU_BLOCK) void k_encode_sizes_lane(
+    const honu_meta *__restrict__ meta, uint64_t var_len, const honu_acl *__restrict__ acl,
+    uint64_t acl_len, const uint32_t *__restrict__ reg, uint64_t reg_len,
+    const uint64_t *__restrict__ payload_off, uint64_t n, uint64_t *__restrict__ sizes,
+    int32_t *__restrict__ status) {
+    const uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const honu_meta &m = meta[i];
+    const uint32_t pr = m.present;
+    uint64_t size = 0;
+    int32_t st = HONU_OK;
+    if (!(pr & HONU_HAS_META)) {
+        st = HONU_ERR_PANIC;  // Marshal(nil, ...): nil deref in Size(), metadata.go:66
+    } else {
+        bool ok = span_in(m.mime.off, m.mime.len, var_len);
+        if (pr & HONU_HAS_SCHEMA) ok = ok && span_in(m.schema_name.off, m.schema_name.len, var_len);
+        if (pr & HONU_HAS_PUBLISHER)
+            ok = ok && span_in(m.ip_address.off, m.ip_address.len, var_len) &&
+                 span_in(m.user_agent.off, m.user_agent.len, var_len);
+        if (pr & HONU_HAS_ENCRYPTION)
+            ok = ok && span_in(m.public_key_id.off, m.public_key_id.len, var_len) &&
+                 span_in(m.encryption_key.off, m.encryption_key.len, var_len) &&
+                 span_in(m.hmac_secret.off, m.hmac_secret.len, var_len) &&
+                 span_in(m.signature.off, m.signature.len, var_len);
+        const uint64_t na = m.acl_count, nr = m.regions_count;
+        const uint64_t ao = m.acl_off, ro = m.regions_off;
+        if (na) ok = ok && ao <= acl_len && na <= acl_len - ao;
+        if (nr) ok = ok && ro <= reg_len && nr <= reg_len - ro;
+        if (!ok) {
+            st = HONU_ERR_INPUT;
+        } else {
+            uint64_t t = 1 + 32;  // meta flag, ObjectID, CollectionID
+            t += 1;               // Version flag
+            if (pr & HONU_HAS_VERSION)
+                t += uvarint_len(m.pid) + uvarint_len(m.vid) + uvarint_len(m.region) + 1 +
+                     ((pr & HONU_HAS_PARENT) ? uvarint_len(m.parent_pid) + uvarint_len(m.parent_vid) : 0) +
+                     1 + uvarint_len(zigzag(m.version_created));
+            t += 1;  // Schema flag
+            if (pr & HONU_HAS_SCHEMA)
+                t += frame_len(m.schema_name.len) + uvarint_len(m.schema_major) +
+                     uvarint_len(m.schema_minor) + uvarint_len(m.schema_patch);
+            t += frame_len(m.mime.len) + 33;  // MIME, Owner, Group, Permissions
+            t += uvarint_len(na);
+            for (uint64_t k = 0; k < na; k++) t += acl[ao + k].present ? 18 : 1;
+            t += uvarint_len(nr);
+            for (uint64_t k = 0; k < nr; k++) t += uvarint_len(reg[ro + k]);
+            t += 3;  // Publisher, Encryption, Compression flags
+            if (pr & HONU_HAS_PUBLISHER) t += 32 + frame_len(m.ip_address.len) + frame_len(m.user_agent.len);
+            if (pr & HONU_HAS_ENCRYPTION)
+                t += frame_len(m.public_key_id.len) + frame_len(m.encryption_key.len) +
+                     frame_len(m.hmac_secret.len) + frame_len(m.signature.len) + 3;
+            if (pr & HONU_HAS_COMPRESSION) t += 1 + uvarint_len(zigzag(m.compression_level));
+            t += 1 + uvarint_len(zigzag(m.created)) + uvarint_len(zigzag(m.modified));
+            const uint64_t dlen = payload_off[i + 1] - payload_off[i];
+            size = 1 + uvarint_len(dlen) + dlen + t;  // object.go:30,35,40
+        }
+    }
+    sizes[i] = size;
+    if (status) status[i] = st;
+}
+
+#undef TRY
+#undef OFF
+
+static dim3 lane_grid(uint64_t n) { return dim3((unsigned)((n + HONU_BLOCK - 1) / HONU_BLOCK)); }
+
+hipError_t launch_decode_parse_lane(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                                    honu_meta *meta, honu_record_info *info,
+                                    DecodeScratch *scratch, uint64_t *counts, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_decode_parse_lane, lane_grid(n), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
+                       meta, info, scratch, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_fill_lane(const uint8_t *rec, uint64_t n, honu_meta *meta,
+                                   honu_record_info *info, const DecodeScratch *scratch,
+                                   const uint64_t *counts, const uint64_t *offs, honu_acl *acl,
+                                   uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap,
+                                   uint8_t *data, uint64_t data_cap, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_decode_fill_lane, lane_grid(n), dim3(HONU_BLOCK), 0, s, rec, n, meta, info,
+                       scratch, counts, offs, acl, acl_cap, reg, reg_cap, data, data_cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_encode_sizes_lane(const honu_meta *meta, uint64_t var_len, const honu_acl *acl,
+                                    uint64_t acl_len, const uint32_t *reg, uint64_t reg_len,
+                                    const uint64_t *payload_off, uint64_t n, uint64_t *sizes,
+                                    int32_t *status, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_encode_sizes_lane, lane_grid(n), dim3(HONU_BLOCK), 0, s, meta, var_len,
+                       acl, acl_len, reg, reg_len, payload_off, n, sizes, status);
+    return hipGetLastError();
+}
+
+}  // namespace honu

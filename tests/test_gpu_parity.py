@@ -20,11 +20,14 @@ from honu_amd.metadata import META_DTYPE, normalize, pack_batch, unpack_row  # n
 from honu_amd.workload import gen_host_batch, gen_meta  # noqa: E402
 
 
-@pytest.fixture(scope="module")
-def codec():
+@pytest.fixture(scope="module", params=[0, 1], ids=["lane", "wave"])
+def codec(request):
+    """Both metadata-kernel variants: one record per lane (default) and one
+    record per wave."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     c = hobj.Codec(0, 1 << 16)
+    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", request.param), "param")
     yield c
     c.close()
 
