@@ -193,8 +193,12 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
         return arg_fail("null pointer");
     if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(launch_encode_meta(ctx->geom, d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
-                              out_cap, d_out_off, d_status, (hipStream_t)stream));
+    if (ctx->geom.record_variant == 0)
+        HIPCHK(launch_encode_meta_lane(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
+                                       out_cap, d_out_off, d_status, (hipStream_t)stream));
+    else
+        HIPCHK(launch_encode_meta(ctx->geom, d_meta, d_var, d_acl, d_regions, d_payload_off, n,
+                                  d_out, out_cap, d_out_off, d_status, (hipStream_t)stream));
     return HONU_OK;
 }
 

@@ -69,6 +69,10 @@ hipError_t launch_decode_fill_lane(const uint8_t *rec, uint64_t n, honu_meta *me
                                    const uint64_t *counts, const uint64_t *offs, honu_acl *acl,
                                    uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap,
                                    uint8_t *data, uint64_t data_cap, hipStream_t s);
+hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
+                                   const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
+                                   uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
+                                   int32_t *status, hipStream_t s);
 hipError_t launch_encode_sizes_lane(const honu_meta *meta, uint64_t var_len, const honu_acl *acl,
                                     uint64_t acl_len, const uint32_t *reg, uint64_t reg_len,
                                     const uint64_t *payload_off, uint64_t n, uint64_t *sizes,

@@ -171,3 +171,109 @@ struct LaneDec {
 };
 
 }  // namespace honu
+
+namespace honu {
+
+// binary.PutUvarint of x as little-endian bytes: lo = bytes 0..7, hi = bytes
+// 8..9; returns the length (1..10). Branch-free LEB128 expansion (the inverse
+// of compact7) with continuation bits on all but the last byte.
+HONU_DEV uint32_t uvarint_bytes(uint64_t x, uint64_t &lo, uint64_t &hi) {
+    const uint32_t n = uvarint_len(x);
+    uint64_t y = x & 0x00FFFFFFFFFFFFFFull;
+    y = (y & 0x000000000FFFFFFFull) | ((y & 0x00FFFFFFF0000000ull) << 4);
+    y = (y & 0x00003FFF00003FFFull) | ((y & 0x0FFFC0000FFFC000ull) << 2);
+    y = (y & 0x007F007F007F007Full) | ((y & 0x3F803F803F803F80ull) << 1);
+    const uint32_t nl = n < 8 ? n : 8;  // bytes in lo
+    const uint64_t cont = n > 8 ? 0x8080808080808080ull
+                                : (0x8080808080808080ull & ((1ull << (8 * (nl - 1))) - 1));
+    lo = (y | cont) & (nl == 8 ? ~0ull : ((1ull << (8 * nl)) - 1));
+    hi = 0;
+    if (n > 8) hi = ((x >> 56) & 0x7F) | (n > 9 ? 0x80 : 0) | ((x >> 63) << 8);
+    return n;
+}
+
+// A lane-private byte stream into global memory at an arbitrary offset. Bytes
+// gather in a 16-byte register chunk aligned to the destination's 16-byte
+// grid; full chunks leave as one 16-byte store, the two partial chunks at the
+// ends as byte stores (their other bytes belong to neighbours).
+struct LaneWriter {
+    uint8_t *out;
+    uint64_t cpos;    // absolute offset of the current chunk (16-aligned)
+    uint32_t f;       // next byte index in the chunk
+    uint32_t first;   // first byte of the chunk this stream owns
+    uint64_t a0, a1;  // chunk bytes 0..7, 8..15
+
+    HONU_DEV void init(uint8_t *o, uint64_t pos) {
+        out = o;
+        cpos = pos & ~15ull;
+        f = first = (uint32_t)(pos & 15);
+        a0 = a1 = 0;
+    }
+    HONU_DEV void store_bytes(uint32_t from, uint32_t to) {
+        for (uint32_t j = from; j < to; j++)
+            out[cpos + j] = (uint8_t)((j < 8 ? a0 >> (8 * j) : a1 >> (8 * (j - 8))) & 0xFF);
+    }
+    HONU_DEV void flush() {
+        if (first == 0)
+            *reinterpret_cast<u32x4 *>(out + cpos) =
+                u32x4{(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32)};
+        else
+            store_bytes(first, 16);
+        first = 0;
+        cpos += 16;
+    }
+    // append the low n (1..8) bytes of v (bytes above n must be zero)
+    HONU_DEV void put(uint64_t v, uint32_t n) {
+        const uint32_t s = 8 * f;
+        uint64_t t2 = 0;
+        if (s < 64) {
+            a0 |= v << s;
+            if (s) a1 |= v >> (64 - s);
+        } else {
+            a1 |= v << (s - 64);
+            if (s > 64) t2 = v >> (128 - s);
+        }
+        f += n;
+        if (f >= 16) {
+            flush();
+            a0 = t2;
+            a1 = 0;
+            f -= 16;
+        }
+    }
+    HONU_DEV void byte(uint32_t v) { put(v & 0xFF, 1); }
+    HONU_DEV void put16(uint64_t lo, uint64_t hi) {
+        put(lo, 8);
+        put(hi, 8);
+    }
+    HONU_DEV void uv(uint64_t x) {
+        uint64_t lo, hi;
+        const uint32_t n = uvarint_bytes(x, lo, hi);
+        put(lo, n < 8 ? n : 8);
+        if (n > 8) put(hi, n - 8);
+    }
+    // raw bytes src[0, len) (global, any alignment, src_end = end of its arena)
+    HONU_DEV void run(const uint8_t *src, uint64_t len) {
+        uint64_t k = 0;
+        const uint64_t a = (uint64_t)src & 7;
+        const uint64_t *w = reinterpret_cast<const uint64_t *>(src - a);
+        for (; k < len; k += 8) {
+            const uint64_t take = len - k < 8 ? len - k : 8;
+            // bytes [a+k, a+k+take) of the aligned word stream
+            const uint64_t q = (a + k) >> 3, sh = (a + k) & 7;
+            uint64_t v = w[q] >> (8 * sh);
+            if (sh && sh + take > 8) v |= w[q + 1] << (64 - 8 * sh);
+            if (take < 8) v &= (1ull << (8 * take)) - 1;
+            put(v, (uint32_t)take);
+        }
+    }
+    HONU_DEV void frame(const uint8_t *var, honu_span sp) {  // lani Encode :62-77
+        uv(sp.len);
+        run(var + sp.off, sp.len);
+    }
+    HONU_DEV void finish() {
+        if (f > first) store_bytes(first, f);
+    }
+};
+
+}  // namespace honu

@@ -312,6 +312,120 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_sizes_lane(
     if (status) status[i] = st;
 }
 
+// ------------------------------------------------------------------------
+// encode: header + Metadata tail (object.go:24-45, metadata.go:108-200)
+// ------------------------------------------------------------------------
+HONU_DEV uint64_t ld64(const uint8_t *p) { return *reinterpret_cast<const uint64_t *>(p); }
+
+__global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
+    const honu_meta *__restrict__ meta, const uint8_t *__restrict__ var,
+    const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
+    const uint64_t *__restrict__ payload_off, uint64_t n, uint8_t *__restrict__ out,
+    uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status) {
+    const uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    if (status[i] != HONU_OK) return;
+    const uint64_t beg = out_off[i], end = out_off[i + 1];
+    if (end > out_cap) {
+        status[i] = HONU_ERR_CAPACITY;
+        return;
+    }
+    const honu_meta &m = meta[i];
+    const uint8_t *mb = reinterpret_cast<const uint8_t *>(&m);
+    const uint32_t pr = m.present;
+    const uint64_t dlen = payload_off[i + 1] - payload_off[i];
+    {  // header: version byte + uvarint(len data)   object.go:30,35
+        uint64_t lo, hi;
+        const uint32_t hn = uvarint_bytes(dlen, lo, hi);
+        out[beg] = HONU_STORAGE_VERSION;
+        for (uint32_t j = 0; j < hn; j++)
+            out[beg + 1 + j] = (uint8_t)(j < 8 ? lo >> (8 * j) : hi >> (8 * (j - 8)));
+    }
+    LaneWriter W;
+    W.init(out, beg + 1 + uvarint_len(dlen) + dlen);
+    W.byte(1);                                                      // EncodeStruct(meta)
+    W.put16(ld64(mb + OFF(object_id)), ld64(mb + OFF(object_id) + 8));          // :110
+    W.put16(ld64(mb + OFF(collection_id)), ld64(mb + OFF(collection_id) + 8));  // :115
+    if (pr & HONU_HAS_VERSION) {                                    // :120, version.go:44-70
+        W.byte(1);
+        W.uv(m.pid);
+        W.uv(m.vid);
+        W.uv(m.region);
+        if (pr & HONU_HAS_PARENT) {
+            W.byte(1);
+            W.uv(m.parent_pid);
+            W.uv(m.parent_vid);
+        } else {
+            W.byte(0);
+        }
+        W.byte(m.tombstone ? 1 : 0);
+        W.uv(zigzag(m.version_created));
+    } else {
+        W.byte(0);
+    }
+    if (pr & HONU_HAS_SCHEMA) {                                     // :125, schema.go:30-53
+        W.byte(1);
+        W.frame(var, m.schema_name);
+        W.uv(m.schema_major);
+        W.uv(m.schema_minor);
+        W.uv(m.schema_patch);
+    } else {
+        W.byte(0);
+    }
+    W.frame(var, m.mime);                                           // :130
+    W.put16(ld64(mb + OFF(owner)), ld64(mb + OFF(owner) + 8));      // :135
+    W.put16(ld64(mb + OFF(group)), ld64(mb + OFF(group) + 8));      // :140
+    W.byte(m.permissions);                                          // :145
+    const uint64_t na = m.acl_count, ao = m.acl_off;
+    W.uv(na);                                                       // :151
+    for (uint64_t k = 0; k < na; k++) {                             // :157-162, acls.go:26-39
+        const uint32_t *a = reinterpret_cast<const uint32_t *>(acl + ao + k);
+        const uint32_t w4 = a[4];
+        if ((w4 >> 8) & 0xFF) {
+            W.byte(1);
+            W.put16(((uint64_t)a[1] << 32) | a[0], ((uint64_t)a[3] << 32) | a[2]);
+            W.byte(w4);
+        } else {
+            W.byte(0);
+        }
+    }
+    const uint64_t nr = m.regions_count, ro = m.regions_off;
+    W.uv(nr);                                                       // :164, region.go:137-152
+    for (uint64_t k = 0; k < nr; k++) W.uv(reg[ro + k]);
+    if (pr & HONU_HAS_PUBLISHER) {                                  // :169, provenance.go:34-57
+        W.byte(1);
+        W.put16(ld64(mb + OFF(publisher_id)), ld64(mb + OFF(publisher_id) + 8));
+        W.put16(ld64(mb + OFF(client_id)), ld64(mb + OFF(client_id) + 8));
+        W.frame(var, m.ip_address);
+        W.frame(var, m.user_agent);
+    } else {
+        W.byte(0);
+    }
+    if (pr & HONU_HAS_ENCRYPTION) {                                 // :174, encryption.go:51-89
+        W.byte(1);
+        W.frame(var, m.public_key_id);
+        W.frame(var, m.encryption_key);
+        W.frame(var, m.hmac_secret);
+        W.frame(var, m.signature);
+        W.byte(m.sealing_alg);
+        W.byte(m.encryption_alg);
+        W.byte(m.signature_alg);
+    } else {
+        W.byte(0);
+    }
+    if (pr & HONU_HAS_COMPRESSION) {                                // :179, compression.go:40-53
+        W.byte(1);
+        W.byte(m.compression_alg);
+        W.uv(zigzag(m.compression_level));
+    } else {
+        W.byte(0);
+    }
+    W.byte(m.flags);                                                // :184
+    W.uv(zigzag(m.created));                                        // :189
+    W.uv(zigzag(m.modified));                                       // :194
+    W.finish();
+}
+
 #undef TRY
 #undef OFF
 
@@ -347,4 +461,16 @@ hipError_t launch_encode_sizes_lane(const honu_meta *meta, uint64_t var_len, con
     return hipGetLastError();
 }
 
+}  // namespace honu
+
+namespace honu {
+hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
+                                   const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
+                                   uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
+                                   int32_t *status, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_encode_meta_lane, lane_grid(n), dim3(HONU_BLOCK), 0, s, meta, var, acl,
+                       reg, payload_off, n, out, out_cap, out_off, status);
+    return hipGetLastError();
+}
 }  // namespace honu
