@@ -179,32 +179,36 @@ HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ s
     const uint64_t tail = n & 15u;
     u32x4 *__restrict__ d4 = reinterpret_cast<u32x4 *>(dst);
     const uint32_t p = (uint32_t)((uint64_t)src & 15u);
+    // Every iteration issues all its loads before any store, with per-chunk
+    // predication instead of a serial remainder loop, so a short segment costs
+    // one round trip, not one per 1 KiB.
     if (p == 0) {
         const u32x4 *__restrict__ s4 = reinterpret_cast<const u32x4 *>(src);
-        uint64_t c = lane;
-        for (; c + (UNROLL - 1) * HONU_WAVE < chunks; c += UNROLL * HONU_WAVE) {
+        for (uint64_t c = lane; c < chunks; c += UNROLL * HONU_WAVE) {
             u32x4 v[UNROLL];
 #pragma unroll
-            for (int u = 0; u < UNROLL; u++) v[u] = ld16<NT>(&s4[c + u * HONU_WAVE]);
+            for (int u = 0; u < UNROLL; u++)
+                if (c + u * HONU_WAVE < chunks) v[u] = ld16<NT>(&s4[c + u * HONU_WAVE]);
 #pragma unroll
-            for (int u = 0; u < UNROLL; u++) st16<NT>(&d4[c + u * HONU_WAVE], v[u]);
+            for (int u = 0; u < UNROLL; u++)
+                if (c + u * HONU_WAVE < chunks) st16<NT>(&d4[c + u * HONU_WAVE], v[u]);
         }
-        for (; c < chunks; c += HONU_WAVE) st16<NT>(&d4[c], ld16<NT>(&s4[c]));
     } else {
         const u32x4 *__restrict__ s4 = reinterpret_cast<const u32x4 *>(src - p);
-        uint64_t c = lane;
-        for (; c + (UNROLL - 1) * HONU_WAVE < chunks; c += UNROLL * HONU_WAVE) {
+        for (uint64_t c = lane; c < chunks; c += UNROLL * HONU_WAVE) {
             u32x4 lo[UNROLL], hi[UNROLL];
 #pragma unroll
             for (int u = 0; u < UNROLL; u++) {
-                lo[u] = ld16<NT>(&s4[c + u * HONU_WAVE]);
-                hi[u] = ld16<NT>(&s4[c + u * HONU_WAVE + 1]);
+                if (c + u * HONU_WAVE < chunks) {
+                    lo[u] = ld16<NT>(&s4[c + u * HONU_WAVE]);
+                    hi[u] = ld16<NT>(&s4[c + u * HONU_WAVE + 1]);
+                }
             }
 #pragma unroll
             for (int u = 0; u < UNROLL; u++)
-                st16<NT>(&d4[c + u * HONU_WAVE], funnel16(lo[u], hi[u], p));
+                if (c + u * HONU_WAVE < chunks)
+                    st16<NT>(&d4[c + u * HONU_WAVE], funnel16(lo[u], hi[u], p));
         }
-        for (; c < chunks; c += HONU_WAVE) st16<NT>(&d4[c], funnel16(ld16<NT>(&s4[c]), ld16<NT>(&s4[c + 1]), p));
     }
     if (tail) {
         const uint64_t t0 = chunks << 4;

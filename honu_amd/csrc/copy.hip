@@ -65,13 +65,20 @@ struct DecodeSegments {
     }
 };
 
+#define SMALL_SEG_WAVES_FACTOR 4
+
 template <class Seg, int UNROLL, bool NT>
 __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t n,
                                                                const uint64_t *__restrict__ total_p) {
-    const uint64_t W = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
+    uint64_t W = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
     const uint64_t w = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + wave_in_block();
     const uint64_t base = seg.lo();
     const uint64_t total = *total_p - base;
+    // Large segments stream best from few waves (DRAM rows stay open: 2 WG per
+    // CU measured best); short segments are latency bound and want every wave
+    // the launch has (SMALL_SEG_WAVES_FACTOR x more).
+    if (n && total / n >= (64u << 10)) W /= SMALL_SEG_WAVES_FACTOR;
+    if (w >= W) return;
     const uint64_t lo = base + ((total * w / W) & ~15ull);
     const uint64_t hi = (w + 1 == W) ? base + total : base + ((total * (w + 1) / W) & ~15ull);
     if (lo >= hi) return;
@@ -161,7 +168,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_sweep(Seg seg, uint64_t n,
 template <class Seg>
 static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
                               const uint64_t *total, hipStream_t s) {
-    const dim3 grid(g.copy_blocks), block(HONU_BLOCK);
+    const dim3 grid(g.copy_blocks * SMALL_SEG_WAVES_FACTOR), block(HONU_BLOCK);
     if (g.copy_variant >= 6) {
         if (!g.tile_map) return hipErrorInvalidValue;
         hipLaunchKernelGGL((k_tile_map<Seg>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,

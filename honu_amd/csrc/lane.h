@@ -252,19 +252,29 @@ struct LaneWriter {
         put(lo, n < 8 ? n : 8);
         if (n > 8) put(hi, n - 8);
     }
-    // raw bytes src[0, len) (global, any alignment, src_end = end of its arena)
+    // raw bytes src[0, len) (global, any alignment). Words are loaded 64 bytes
+    // at a time before any of them is written out: the output stores may
+    // alias for the compiler, so loads cannot move past them on their own.
     HONU_DEV void run(const uint8_t *src, uint64_t len) {
-        uint64_t k = 0;
         const uint64_t a = (uint64_t)src & 7;
         const uint64_t *w = reinterpret_cast<const uint64_t *>(src - a);
-        for (; k < len; k += 8) {
-            const uint64_t take = len - k < 8 ? len - k : 8;
-            // bytes [a+k, a+k+take) of the aligned word stream
-            const uint64_t q = (a + k) >> 3, sh = (a + k) & 7;
-            uint64_t v = w[q] >> (8 * sh);
-            if (sh && sh + take > 8) v |= w[q + 1] << (64 - 8 * sh);
-            if (take < 8) v &= (1ull << (8 * take)) - 1;
-            put(v, (uint32_t)take);
+        const uint64_t nw = (a + len + 7) >> 3;  // aligned words holding the run
+        for (uint64_t k = 0; k < len; k += 64) {
+            const uint64_t q0 = (a + k) >> 3;
+            uint64_t x[9];
+#pragma unroll
+            for (int j = 0; j < 9; j++) x[j] = (q0 + j < nw) ? w[q0 + j] : 0;
+            const uint32_t sh = (uint32_t)(a & 7) * 8;  // same phase every batch
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint64_t off = k + 8 * j;
+                if (off < len) {
+                    const uint64_t take = len - off < 8 ? len - off : 8;
+                    uint64_t v = sh ? (x[j] >> sh) | (x[j + 1] << (64 - sh)) : x[j];
+                    if (take < 8) v &= (1ull << (8 * take)) - 1;
+                    put(v, (uint32_t)take);
+                }
+            }
         }
     }
     HONU_DEV void frame(const uint8_t *var, honu_span sp) {  // lani Encode :62-77

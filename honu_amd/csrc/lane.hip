@@ -111,13 +111,34 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_lane(
             if (nacl > 0) {                                     // :254-265
                 if (nacl > GO_MAX_ALLOC / 8) TRY(HONU_ERR_PANIC);  // make([]*AccessControl)
                 acl_pos = D.p;
-                for (uint64_t k = 0; k < nacl; k++) {           // acls.go:41-51
-                    TRY(D.boolean(f));
-                    if (f) {
-                        if (D.p >= D.end) TRY(HONU_ERR_EOF);
-                        if (D.p + 16 > D.end) TRY(HONU_ERR_UNEXPECTED_EOF);
-                        D.p += 16;
-                        TRY(D.u8(u));
+                // acls.go:41-51. Speculate that entries are present: the next
+                // 8 flags then sit at p + 18j and load independently; the walk
+                // checks them in order and re-speculates after a nil entry.
+                for (uint64_t k = 0; k < nacl;) {
+                    uint32_t fl[8];
+                    const uint64_t p0 = D.p;
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        const uint64_t q = p0 + 18 * j;
+                        fl[j] = (k + j < nacl && q < D.end) ? rec[q] : 0;
+                    }
+                    bool stop = false;
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        if (k < nacl && !stop) {
+                            if (D.p >= D.end) TRY(HONU_ERR_EOF);     // DecodeBool
+                            if (fl[j] > 1) TRY(HONU_ERR_PARSE_BOOLEAN);
+                            if (fl[j]) {
+                                if (D.p + 1 >= D.end) TRY(HONU_ERR_EOF);             // DecodeULID
+                                if (D.p + 17 > D.end) TRY(HONU_ERR_UNEXPECTED_EOF);
+                                if (D.p + 17 >= D.end) TRY(HONU_ERR_EOF);            // DecodeUint8
+                                D.p += 18;
+                            } else {
+                                D.p += 1;
+                                stop = true;
+                            }
+                            k++;
+                        }
                     }
                 }
                 R.u64(OFF(acl_count), nacl);
@@ -204,19 +225,45 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_lane(
             const DecodeScratch sc = scratch[i];
             const uint64_t end = sc.rec_end;
             uint64_t p = sc.acl_pos;
-            for (uint64_t k = 0; k < na; k++) {  // validated by the parse
-                uint32_t *e = reinterpret_cast<uint32_t *>(acl + ao + k);
-                if (rec[p]) {
-                    uint64_t lo, hi;
-                    lane_fetch16(rec, p + 1, end, lo, hi);
-                    e[0] = (uint32_t)lo;
-                    e[1] = (uint32_t)(lo >> 32);
-                    e[2] = (uint32_t)hi;
-                    e[3] = (uint32_t)(hi >> 32);
-                    e[4] = (uint32_t)rec[p + 17] | (1u << 8);
-                    p += 18;
-                } else {
+            // entries validated by the parse; speculate 8 present entries at a
+            // time (flags at p + 18j) so their loads issue together
+            for (uint64_t k = 0; k < na;) {
+                uint32_t fl[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const uint64_t q = p + 18 * j;
+                    fl[j] = (k + j < na && q < end) ? rec[q] : 0;
+                }
+                uint32_t run = 0;  // leading present entries
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if (run == (uint32_t)j && fl[j] == 1 && k + j < na) run = j + 1;
+                uint64_t lo[8], hi[8];
+                uint32_t pm[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    if ((uint32_t)j < run) {
+                        lane_fetch16(rec, p + 18 * j + 1, end, lo[j], hi[j]);
+                        pm[j] = rec[p + 18 * j + 17];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    if ((uint32_t)j < run) {
+                        uint32_t *e = reinterpret_cast<uint32_t *>(acl + ao + k + j);
+                        e[0] = (uint32_t)lo[j];
+                        e[1] = (uint32_t)(lo[j] >> 32);
+                        e[2] = (uint32_t)hi[j];
+                        e[3] = (uint32_t)(hi[j] >> 32);
+                        e[4] = pm[j] | (1u << 8);
+                    }
+                }
+                k += run;
+                p += 18 * (uint64_t)run;
+                if (run < 8 && k < na) {  // a nil entry: one 0x00 flag byte
+                    uint32_t *e = reinterpret_cast<uint32_t *>(acl + ao + k);
                     e[0] = e[1] = e[2] = e[3] = e[4] = 0;
+                    k += 1;
                     p += 1;
                 }
             }
@@ -330,7 +377,14 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
         status[i] = HONU_ERR_CAPACITY;
         return;
     }
-    const honu_meta &m = meta[i];
+    // the whole row in registers first (loads cannot pass the output stores)
+    honu_meta m;
+    {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(meta + i);
+        u32x4 *dstr = reinterpret_cast<u32x4 *>(&m);
+#pragma unroll
+        for (int k = 0; k < 22; k++) dstr[k] = src[k];
+    }
     const uint8_t *mb = reinterpret_cast<const uint8_t *>(&m);
     const uint32_t pr = m.present;
     const uint64_t dlen = payload_off[i + 1] - payload_off[i];
@@ -378,20 +432,39 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
     W.byte(m.permissions);                                          // :145
     const uint64_t na = m.acl_count, ao = m.acl_off;
     W.uv(na);                                                       // :151
-    for (uint64_t k = 0; k < na; k++) {                             // :157-162, acls.go:26-39
-        const uint32_t *a = reinterpret_cast<const uint32_t *>(acl + ao + k);
-        const uint32_t w4 = a[4];
-        if ((w4 >> 8) & 0xFF) {
-            W.byte(1);
-            W.put16(((uint64_t)a[1] << 32) | a[0], ((uint64_t)a[3] << 32) | a[2]);
-            W.byte(w4);
-        } else {
-            W.byte(0);
+    for (uint64_t k0 = 0; k0 < na; k0 += 8) {                       // :157-162, acls.go:26-39
+        uint32_t e[8][5];                                            // 8 entries ahead
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if (k0 + j < na) {
+                const uint32_t *a = reinterpret_cast<const uint32_t *>(acl + ao + k0 + j);
+#pragma unroll
+                for (int c = 0; c < 5; c++) e[j][c] = a[c];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if (k0 + j < na) {
+                if ((e[j][4] >> 8) & 0xFF) {
+                    W.byte(1);
+                    W.put16(((uint64_t)e[j][1] << 32) | e[j][0], ((uint64_t)e[j][3] << 32) | e[j][2]);
+                    W.byte(e[j][4]);
+                } else {
+                    W.byte(0);
+                }
+            }
         }
     }
     const uint64_t nr = m.regions_count, ro = m.regions_off;
     W.uv(nr);                                                       // :164, region.go:137-152
-    for (uint64_t k = 0; k < nr; k++) W.uv(reg[ro + k]);
+    for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
+        uint32_t r8[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? reg[ro + k0 + j] : 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (k0 + j < nr) W.uv(r8[j]);
+    }
     if (pr & HONU_HAS_PUBLISHER) {                                  // :169, provenance.go:34-57
         W.byte(1);
         W.put16(ld64(mb + OFF(publisher_id)), ld64(mb + OFF(publisher_id) + 8));
