@@ -46,7 +46,10 @@ def parse_args():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--records", type=int, default=1 << 20, help="records per GPU")
     p.add_argument("--shape", default="large")
-    p.add_argument("--chunk", type=int, default=1 << 16)
+    p.add_argument("--chunk-gib", type=float, default=12.0,
+                   help="encoded bytes per device-resident chunk (output slots are sized by it)")
+    p.add_argument("--min-chunks", type=int, default=4,
+                   help="at least this many chunks, so metadata and copies can overlap")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--cpu-records", type=int, default=2048)
@@ -80,8 +83,6 @@ class Bench:
     def __init__(self, args, rank, device):
         self.args = args
         self.dev = torch.device("cuda", device)
-        self.codec = Codec(device, max_records=args.chunk)
-        self.lib = self.codec.lib
         N = args.records
         self.N = N
         self.first = rank * N
@@ -90,6 +91,20 @@ class Bench:
         self.host_meta = meta
         self.host_off = off
         self.gen_s = time.time() - t0
+        # chunk boundaries by bytes (payload + ~1.1 KB of header/metadata per record)
+        est = np.diff(off.astype(np.int64)) + 1100
+        cum = np.concatenate([[0], np.cumsum(est)])
+        budget = min(args.chunk_gib * 2**30, cum[-1] / max(1, args.min_chunks) + 1)
+        bounds = [0]
+        while bounds[-1] < N:
+            a = bounds[-1]
+            b = int(np.searchsorted(cum, cum[a] + budget, side="right")) - 1
+            bounds.append(min(N, max(b, a + 1)))
+        self.chunks = list(zip(bounds[:-1], bounds[1:]))
+        C = max(b - a for a, b in self.chunks)
+        self.C = C
+        self.codec = Codec(device, max_records=C)
+        self.lib = self.codec.lib
 
         def D(a):
             a = np.ascontiguousarray(a)
@@ -105,8 +120,6 @@ class Bench:
         s0 = torch.cuda.current_stream(self.dev).cuda_stream
         _lib.check(self.lib.honu_gen_payload(self.codec.ctx, args.seed, self.first, N, P(self.off),
                                              P(self.payload), s0), "gen_payload")
-        self.chunks = [(a, min(a + args.chunk, N)) for a in range(0, N, args.chunk)]
-        C = args.chunk
         # sizing pass (untimed): exact record bytes of every chunk
         out_off = torch.empty(8 * (C + 1), dtype=torch.uint8, device=self.dev)
         status = torch.empty(4 * C + 16, dtype=torch.uint8, device=self.dev)
@@ -238,7 +251,7 @@ class Bench:
         return bool(ok)
 
 
-def copy_peak_gbs(dev, nbytes=8 << 30, reps=5):
+def copy_peak_gbs(dev, nbytes=4 << 30, reps=5):
     """Achievable HBM copy rate on this device (torch copy_), read+write bytes."""
     a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     b = torch.empty_like(a)
@@ -374,7 +387,8 @@ def main():
                         "materialising decode (Object.Metadata + Object.Data)",
             "records_per_gpu": bench.N,
             "shape": args.shape,
-            "chunk_records": args.chunk,
+            "chunks": len(bench.chunks),
+            "chunk_records_max": bench.C,
             "encoded_bytes_per_gpu": bench.total_rec_bytes,
             "payload_bytes_per_gpu": bench.payload_bytes,
             "parallelism": f"dp{world} (records sharded, no data-path collective)",

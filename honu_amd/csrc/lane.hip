@@ -341,9 +341,21 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_sizes_lane(
                      uvarint_len(m.schema_minor) + uvarint_len(m.schema_patch);
             t += frame_len(m.mime.len) + 33;  // MIME, Owner, Group, Permissions
             t += uvarint_len(na);
-            for (uint64_t k = 0; k < na; k++) t += acl[ao + k].present ? 18 : 1;
+            for (uint64_t k0 = 0; k0 < na; k0 += 8) {  // 8 independent loads per round
+                uint32_t pz[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) pz[j] = k0 + j < na ? acl[ao + k0 + j].present : 2;
+#pragma unroll
+                for (int j = 0; j < 8; j++) t += pz[j] == 2 ? 0 : (pz[j] ? 18 : 1);
+            }
             t += uvarint_len(nr);
-            for (uint64_t k = 0; k < nr; k++) t += uvarint_len(reg[ro + k]);
+            for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
+                uint32_t r8[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? reg[ro + k0 + j] : 0;
+#pragma unroll
+                for (int j = 0; j < 8; j++) t += k0 + j < nr ? uvarint_len(r8[j]) : 0;
+            }
             t += 3;  // Publisher, Encryption, Compression flags
             if (pr & HONU_HAS_PUBLISHER) t += 32 + frame_len(m.ip_address.len) + frame_len(m.user_agent.len);
             if (pr & HONU_HAS_ENCRYPTION)
