@@ -364,10 +364,20 @@ def main():
     total_records = bench.N * world
     total_bytes = bench.total_rec_bytes * world
     launches = len(dec_ms)
-    dom_ms, dom_gbs, dom_name = (sum(dec_ms), dec_gbs, "k_copy_segments<DecodeSegments>")
+    dom_ms, dom_gbs, dom_name = (sum(dec_ms), dec_gbs, "k_copy_segments<honu::DecodeSegments>")
     if sum(enc_ms) > sum(dec_ms):
-        dom_ms, dom_gbs, dom_name = (sum(enc_ms), enc_gbs, "k_copy_segments<EncodeSegments>")
+        dom_ms, dom_gbs, dom_name = (sum(enc_ms), enc_gbs, "k_copy_segments<honu::EncodeSegments>")
     peak_meas = copy_peak_gbs(bench.dev)
+    workload = (f"{bench.N} {args.shape} records per GPU: encode (object.Marshal) + "
+                "materialising decode (Object.Metadata + Object.Data)")
+    traffic, traffic_src = None, None
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tpath):  # PMC passes of this same command (tools/pmc_traffic.py)
+        pm = json.load(open(tpath))
+        kn = dom_name.split("<")[0] + "<" + dom_name.split("<")[1].split(">")[0]
+        for k, v in pm.get("kernels", {}).items():
+            if pm.get("workload") == workload and k.startswith("void honu::" + kn):
+                traffic, traffic_src = v["traffic_per_launch"], "profiles/pmc_traffic.json"
     result = {
         "metric": METRIC,
         "value": total_bytes / step_s / 2**30,
@@ -383,8 +393,7 @@ def main():
         "data": "synthetic: seeded generator mirroring object_test.go:195-386, payload bytes "
                 "generated on device",
         "config": {
-            "workload": f"{bench.N} {args.shape} records per GPU: encode (object.Marshal) + "
-                        "materialising decode (Object.Metadata + Object.Data)",
+            "workload": workload,
             "records_per_gpu": bench.N,
             "shape": args.shape,
             "chunks": len(bench.chunks),
@@ -403,7 +412,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": dom_gbs / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "launches": launches,
             "avg_launch_ms": dom_ms / launches,
             "algorithmic_bytes_per_launch": sum(enc_bytes) / launches,
