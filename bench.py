@@ -33,7 +33,8 @@ sys.path.insert(0, ROOT)
 
 from honu_amd import _lib  # noqa: E402
 from honu_amd.object import Codec  # noqa: E402
-from honu_amd.workload import gen_meta, shape_id  # noqa: E402
+from honu_amd.shard import weak_range  # noqa: E402
+from honu_amd.workload import gen_meta  # noqa: E402
 
 METRIC = "GiB/s + records/s device-resident encode+decode, 1M Large(~300KB) object batch"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -85,7 +86,7 @@ class Bench:
         self.dev = torch.device("cuda", device)
         N = args.records
         self.N = N
-        self.first = rank * N
+        self.first, _ = weak_range(rank, int(os.environ.get("WORLD_SIZE", "1")), N)
         t0 = time.time()
         meta, var, acl, reg, off = gen_meta(args.seed, args.shape, self.first, N)
         self.host_meta = meta
