@@ -110,8 +110,8 @@ def decode_batch(rec: np.ndarray, rec_off: np.ndarray, materialize: bool = False
     nbytes = int(rec_off[-1]) if n >= 0 else 0
     meta = np.zeros(max(n, 1), META_DTYPE)
     info = np.zeros(max(n, 1), INFO_DTYPE)
-    acl = np.zeros(max(nbytes, 1), ACL_DTYPE)
-    reg = np.zeros(max(nbytes, 1), np.uint32)
+    acl = np.zeros(nbytes + 1, ACL_DTYPE)  # lazily zeroed; a nil entry is 1 byte
+    reg = np.zeros(nbytes + 1, np.uint32)
     data = np.zeros(nbytes + 16 * n + 16, np.uint8) if materialize else None
     totals = np.zeros(3, np.uint64)
     lib.oracle_decode_batch(_p(rec), _p(rec_off), n, _p(meta), _p(info), _p(acl), len(acl),
