@@ -395,11 +395,11 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill(
                 Win w;
                 w.L = win_lds[wib];
                 w.rec = rec;
-                const uint64_t lists_end = sc.regions_pos + 5 * nr;  // never past the lists
+                const uint64_t lists_end = (sc.regions_pos & GRP_POS_MASK) + 5 * nr;  // never past the lists
                 w.end = lists_end < sc.rec_end ? lists_end : sc.rec_end;
                 w.lo = 1;
                 w.hi = 0;
-                uint64_t p = sc.acl_pos;
+                uint64_t p = sc.acl_pos & GRP_POS_MASK;
                 for (uint64_t i = 0; i < na; i++) {  // entries validated by the parse
                     w.ensure(p, 18);
                     const uint8_t flag = w.at(p);
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill(
                     }
                     p += flag ? 18 : 1;
                 }
-                p = sc.regions_pos;
+                p = sc.regions_pos & GRP_POS_MASK;
                 for (uint64_t i = 0; i < nr; i++) {
                     w.ensure(p, 5);
                     uint64_t x = 0;

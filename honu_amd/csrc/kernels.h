@@ -21,12 +21,21 @@ struct DecodeScratch {
     uint64_t rec_end;     // absolute end of the record
 };
 
+// Flag bits on DecodeScratch::acl_pos / regions_pos, set by the lane and group
+// parses for the group fill (positions are < 2^62).
+#define GRP_ACL_FAST (1ull << 63)    // acl_pos: every entry present, entry j at acl_pos + 18 j
+#define GRP_REG_INLINE (1ull << 62)  // regions_pos: region ids in reg_inline[8 i ..]
+#define GRP_POS_MASK (~(GRP_ACL_FAST | GRP_REG_INLINE))
+
 struct LaunchGeom {
     int num_cu;
     int per_record_blocks;  // cap on blocks for one-wave-per-record kernels
     int copy_blocks;        // blocks of the byte-balanced copy kernel
     int copy_variant;       // copy engine variant (copy.hip: unroll depth / cache policy)
-    int record_variant;     // 0: one record per lane (lane.hip), 1: one record per wave
+    int record_variant;     // per-record kernels: 0 auto (group size pass and fill,
+                            // lane encode and parse), 1 one record per wave,
+                            // 2 one record per group of 16 lanes (grp.hip),
+                            // 3 one record per lane (lane.hip)
     uint32_t *tile_map;     // sweep-form tile -> segment map (context scratch)
     uint64_t tile_map_cap;
 };
@@ -63,7 +72,8 @@ hipError_t launch_decode_keys(const LaunchGeom &g, const honu_meta *meta,
 
 hipError_t launch_decode_parse_lane(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                     honu_meta *meta, honu_record_info *info,
-                                    DecodeScratch *scratch, uint64_t *counts, hipStream_t s);
+                                    DecodeScratch *scratch, uint32_t *reg_inline,
+                                    uint64_t *counts, hipStream_t s);
 hipError_t launch_decode_fill_lane(const uint8_t *rec, uint64_t n, honu_meta *meta,
                                    honu_record_info *info, const DecodeScratch *scratch,
                                    const uint64_t *counts, const uint64_t *offs, honu_acl *acl,
@@ -77,6 +87,25 @@ hipError_t launch_encode_sizes_lane(const honu_meta *meta, uint64_t var_len, con
                                     uint64_t acl_len, const uint32_t *reg, uint64_t reg_len,
                                     const uint64_t *payload_off, uint64_t n, uint64_t *sizes,
                                     int32_t *status, hipStream_t s);
+
+hipError_t launch_encode_sizes_grp(const honu_meta *meta, uint64_t var_len, const honu_acl *acl,
+                                   uint64_t acl_len, const uint32_t *reg, uint64_t reg_len,
+                                   const uint64_t *payload_off, uint64_t n, uint64_t *sizes,
+                                   int32_t *status, hipStream_t s);
+hipError_t launch_encode_meta_grp(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
+                                  const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
+                                  uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
+                                  int32_t *status, hipStream_t s);
+hipError_t launch_decode_parse_grp(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                                   honu_meta *meta, honu_record_info *info,
+                                   DecodeScratch *scratch, uint32_t *reg_inline, uint64_t *counts,
+                                   hipStream_t s);
+hipError_t launch_decode_fill_grp(const uint8_t *rec, uint64_t n, honu_meta *meta,
+                                  honu_record_info *info, const DecodeScratch *scratch,
+                                  const uint32_t *reg_inline, const uint64_t *counts,
+                                  const uint64_t *offs, honu_acl *acl, uint64_t acl_cap,
+                                  uint32_t *reg, uint64_t reg_cap, uint8_t *data,
+                                  uint64_t data_cap, hipStream_t s);
 
 // Exclusive scan of K interleaved u64 columns: out[i*K+c] = sum_{j<i} in[j*K+c];
 // totals[c] = full sum. `partials` needs scan_partials_len(n, K) u64.

@@ -18,16 +18,10 @@
 
 namespace honu {
 
-// Bytes [q, q+16) of the arena as two little-endian u64 (bytes at or beyond
-// `end` are unspecified). Requires q < end. The second aligned block is read
-// only when it holds a byte below `end`, so no load leaves mapped memory.
-HONU_DEV void lane_fetch16(const uint8_t *__restrict__ base, uint64_t q, uint64_t end,
-                           uint64_t &lo, uint64_t &hi) {
-    const uint64_t A = q & ~15ull;
-    const uint32_t s = (uint32_t)(q & 15);
-    const u32x4 a = *reinterpret_cast<const u32x4 *>(base + A);
-    u32x4 b = {0, 0, 0, 0};
-    if (s && A + 16 < end) b = *reinterpret_cast<const u32x4 *>(base + A + 16);
+// Bytes [s, s+16) of the 32-byte window a||b (s in [0,16)) as two
+// little-endian u64: five word picks by the per-lane word offset, then one
+// v_alignbyte per output word.
+HONU_DEV void window16(const u32x4 a, const u32x4 b, uint32_t s, uint64_t &lo, uint64_t &hi) {
     const uint32_t q4 = s >> 2, sh = s & 3;
     // w[k] = word k of a||b; pick(j) = w[q4 + j] for j in 0..4 (per-lane q4)
     const uint32_t w0 = a.x, w1 = a.y, w2 = a.z, w3 = a.w, w4 = b.x, w5 = b.y, w6 = b.z, w7 = b.w;
@@ -45,6 +39,19 @@ HONU_DEV void lane_fetch16(const uint8_t *__restrict__ base, uint64_t q, uint64_
     const uint32_t r3 = __builtin_amdgcn_alignbyte(p4, p3, sh);
     lo = ((uint64_t)r1 << 32) | r0;
     hi = ((uint64_t)r3 << 32) | r2;
+}
+
+// Bytes [q, q+16) of the arena as two little-endian u64 (bytes at or beyond
+// `end` are unspecified). Requires q < end. The second aligned block is read
+// only when it holds a byte below `end`, so no load leaves mapped memory.
+HONU_DEV void lane_fetch16(const uint8_t *__restrict__ base, uint64_t q, uint64_t end,
+                           uint64_t &lo, uint64_t &hi) {
+    const uint64_t A = q & ~15ull;
+    const uint32_t s = (uint32_t)(q & 15);
+    const u32x4 a = *reinterpret_cast<const u32x4 *>(base + A);
+    u32x4 b = {0, 0, 0, 0};
+    if (s && A + 16 < end) b = *reinterpret_cast<const u32x4 *>(base + A + 16);
+    window16(a, b, s, lo, hi);
 }
 
 // Compact the 7-bit groups of up to 8 varint bytes (top bits already clear).

@@ -21,7 +21,8 @@ namespace honu {
 __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_lane(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
     honu_meta *__restrict__ meta, honu_record_info *__restrict__ info,
-    DecodeScratch *__restrict__ scratch, uint64_t *__restrict__ counts) {
+    DecodeScratch *__restrict__ scratch, uint32_t *__restrict__ reg_inline,
+    uint64_t *__restrict__ counts) {
     const uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint64_t beg = rec_off[i], end = rec_off[i + 1];
@@ -114,6 +115,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_lane(
                 // acls.go:41-51. Speculate that entries are present: the next
                 // 8 flags then sit at p + 18j and load independently; the walk
                 // checks them in order and re-speculates after a nil entry.
+                bool all_present = true;
                 for (uint64_t k = 0; k < nacl;) {
                     uint32_t fl[8];
                     const uint64_t p0 = D.p;
@@ -136,18 +138,24 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_lane(
                             } else {
                                 D.p += 1;
                                 stop = true;
+                                all_present = false;
                             }
                             k++;
                         }
                     }
                 }
                 R.u64(OFF(acl_count), nacl);
+                if (all_present) acl_pos |= GRP_ACL_FAST;  // for the group fill
             }
             TRY(D.u64(nreg));                                   // region.go:154-169
             if (nreg > GO_MAX_ALLOC / 4) TRY(HONU_ERR_PANIC);   // make(Regions, length)
             pr |= HONU_REGIONS_NONNIL;
             reg_pos = D.p;
-            for (uint64_t k = 0; k < nreg; k++) TRY(D.u32(u));
+            for (uint64_t k = 0; k < nreg; k++) {
+                TRY(D.u32(u));
+                if (k < 8) reg_inline[8 * i + k] = u;
+            }
+            if (nreg <= 8) reg_pos |= GRP_REG_INLINE;
             R.u64(OFF(regions_count), nreg);
             TRY(D.boolean(f));                                  // :271 Publisher
             if (f) {
@@ -224,7 +232,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_lane(
         } else if (na + nr) {
             const DecodeScratch sc = scratch[i];
             const uint64_t end = sc.rec_end;
-            uint64_t p = sc.acl_pos;
+            uint64_t p = sc.acl_pos & GRP_POS_MASK;
             // entries validated by the parse; speculate 8 present entries at a
             // time (flags at p + 18j) so their loads issue together
             for (uint64_t k = 0; k < na;) {
@@ -267,7 +275,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_lane(
                     p += 1;
                 }
             }
-            p = sc.regions_pos;
+            p = sc.regions_pos & GRP_POS_MASK;
             for (uint64_t k = 0; k < nr; k++) {
                 const uint64_t avail = end - p;
                 uint64_t lo, hi, v = 0;
@@ -518,10 +526,11 @@ static dim3 lane_grid(uint64_t n) { return dim3((unsigned)((n + HONU_BLOCK - 1) 
 
 hipError_t launch_decode_parse_lane(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                     honu_meta *meta, honu_record_info *info,
-                                    DecodeScratch *scratch, uint64_t *counts, hipStream_t s) {
+                                    DecodeScratch *scratch, uint32_t *reg_inline,
+                                    uint64_t *counts, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_decode_parse_lane, lane_grid(n), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
-                       meta, info, scratch, counts);
+                       meta, info, scratch, reg_inline, counts);
     return hipGetLastError();
 }
 

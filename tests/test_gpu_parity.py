@@ -20,10 +20,10 @@ from honu_amd.metadata import META_DTYPE, normalize, pack_batch, unpack_row  # n
 from honu_amd.workload import gen_host_batch, gen_meta  # noqa: E402
 
 
-@pytest.fixture(scope="module", params=[0, 1], ids=["lane", "wave"])
+@pytest.fixture(scope="module", params=[0, 1, 2, 3], ids=["auto", "wave", "group", "lane"])
 def codec(request):
-    """Both metadata-kernel variants: one record per lane (default) and one
-    record per wave."""
+    """Every metadata-kernel variant: auto (the default per-kernel choice), one
+    record per wave, per group of 16 lanes, per lane."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     c = hobj.Codec(0, 1 << 16)
@@ -272,3 +272,58 @@ def test_full_size_property_large(codec, oracle_lib):
     assert np.array_equal(goff, ooff)
     for i in sample:
         assert out[int(goff[i]):int(goff[i + 1])].tobytes() == oout[int(ooff[i]):int(ooff[i + 1])].tobytes()
+
+
+def _odd_metas(seed=11, n=48):
+    """Records outside the generator's envelope: tails beyond one 2 KiB LDS
+    window (long frames, hundreds of ACL entries), nil ACL entries, more than
+    8 regions, multi-byte region varints, empty and nil lists."""
+    from honu_amd.metadata import (AccessControl, Compression, Encryption, Metadata, Publisher,
+                                   Scalar, SchemaVersion, Version)
+    rng = np.random.default_rng(seed)
+    metas, datas = [], []
+    for i in range(n):
+        kind = i % 6
+        nacl = [0, 3, 130, 300, 17, 64][kind]
+        acl = None if nacl == 0 else [
+            None if (kind in (1, 3, 4) and j % 7 == 3) else
+            AccessControl(rng.bytes(16), int(rng.integers(0, 256))) for j in range(nacl)]
+        regs = [int(x) for x in rng.integers(0, [2**7, 2**14, 2**21, 2**32, 2**32, 2**10][kind],
+                                              [0, 5, 9, 40, 8, 12][kind])]
+        sig = rng.bytes([0, 32, 5000, 300, 2100, 1][kind])
+        m = Metadata(
+            ObjectID=rng.bytes(16), CollectionID=rng.bytes(16),
+            Version=Version(Scalar(int(rng.integers(0, 2**32)), int(rng.integers(0, 2**63))),
+                            int(rng.integers(0, 2**32)), Scalar(7, 9) if kind % 2 else None,
+                            bool(kind & 2), int(rng.integers(-2**62, 2**62))),
+            Schema=SchemaVersion("S" * [0, 3, 700, 20, 5, 1][kind], 1, 2**20, 3) if kind else None,
+            MIME="m" * [0, 10, 3000, 17, 40, 2][kind], Owner=rng.bytes(16), Group=rng.bytes(16),
+            Permissions=int(rng.integers(0, 256)), ACL=acl,
+            WriteRegions=regs if kind != 0 else None,
+            Publisher=Publisher(rng.bytes(16), rng.bytes(16), rng.bytes(16),
+                                "UA" * [0, 5, 900, 1, 3, 7][kind]) if kind != 5 else None,
+            Encryption=Encryption("k" * 22, rng.bytes(32), rng.bytes(32), sig, 1, 2, 4)
+            if kind != 1 else None,
+            Compression=Compression(1, int(rng.integers(-5, 10))) if kind % 3 else None,
+            Flags=int(rng.integers(0, 256)), Created=int(rng.integers(0, 2**62)),
+            Modified=int(rng.integers(0, 2**62)))
+        metas.append(m)
+        datas.append(rng.bytes(int(rng.integers(0, 3000))) if i % 5 else None)
+    return metas, datas
+
+
+def test_long_tails_and_nil_entries_parity(codec, oracle_lib):
+    metas, datas = _odd_metas()
+    hb = pack_batch(metas, datas)
+    out, off, st = gpu_marshal(codec, hb)
+    oout, ooff, ost = oracle_lib.marshal_batch(hb)
+    assert np.array_equal(st, ost) and (st == 0).all()
+    assert np.array_equal(off, ooff)
+    assert out.tobytes() == oout.tobytes()
+    tails = np.diff(off.astype(np.int64))
+    assert tails.max() > 3 * 2048  # several stage windows
+    for materialize in (False, True):
+        meta, info, acl, reg, data = assert_decode_equal(oracle_lib, codec, oout, ooff, materialize)
+        assert (info["meta_status"] == 0).all()
+    for i in range(len(metas)):
+        assert unpack_row(meta[i], oout, acl, reg) == normalize(metas[i]), i
