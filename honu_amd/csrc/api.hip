@@ -23,6 +23,7 @@ struct honu_ctx {
     uint64_t *partials;      // scan partials
     DecodeScratch *scratch;  // max_n
     uint32_t *reg_inline;    // 8 * max_n: region ids handed from the group parse to fill
+    uint64_t *enc_acl;       // max_n: ACL list positions, lane encoder -> group ACL encoder
 };
 
 static thread_local char g_last_error[256];
@@ -112,7 +113,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     const uint64_t np = scan_partials_len(n, 3) + scan_partials_len(n, 1);
     const uint64_t map_cap = 1ull << 22;  // tile map entries (sweep copy variants)
     const uint64_t bytes =
-        8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 32 * n + 4 * map_cap + 256;
+        8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 32 * n + 8 * n + 4 * map_cap + 256;
     if (hipMalloc(&c->ws, bytes) != hipSuccess) {
         snprintf(g_last_error, sizeof g_last_error, "hipMalloc(%llu) failed",
                  (unsigned long long)bytes);
@@ -131,7 +132,8 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     w += np;
     c->scratch = (DecodeScratch *)w;
     c->reg_inline = (uint32_t *)(c->scratch + n);
-    c->geom.tile_map = c->reg_inline + 8 * n;
+    c->enc_acl = (uint64_t *)(c->reg_inline + 8 * n);
+    c->geom.tile_map = (uint32_t *)(c->enc_acl + n);
     c->geom.tile_map_cap = map_cap;
     return c;
 }
@@ -167,7 +169,7 @@ int32_t honu_encode_sizes(honu_ctx *ctx, const honu_meta *d_meta, uint64_t var_l
     if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
     HIPCHK(hipSetDevice(ctx->device));
     const int rv = ctx->geom.record_variant;
-    if (rv == 0 || rv == 2)
+    if (rv == 0 || rv == 2 || rv == 4)
         HIPCHK(launch_encode_sizes_grp(d_meta, var_len, d_acl, acl_len, d_regions, regions_len,
                                        d_payload_off, n, d_sizes, d_status, (hipStream_t)stream));
     else if (rv == 3)
@@ -203,10 +205,18 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
     if (rv == 2)
         HIPCHK(launch_encode_meta_grp(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
                                       out_cap, d_out_off, d_status, (hipStream_t)stream));
-    else if (rv == 0 || rv == 3)
+    else if (rv == 3 || rv == 4)
         HIPCHK(launch_encode_meta_lane(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
-                                       out_cap, d_out_off, d_status, (hipStream_t)stream));
-    else
+                                       out_cap, d_out_off, d_status, nullptr,
+                                       (hipStream_t)stream));
+    else if (rv == 0) {
+        if (n > ctx->max_n) return HONU_E_WORKSPACE;
+        HIPCHK(launch_encode_meta_lane(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
+                                       out_cap, d_out_off, d_status, ctx->enc_acl,
+                                       (hipStream_t)stream));
+        HIPCHK(launch_encode_acl_grp(d_meta, d_acl, n, d_out, d_status, ctx->enc_acl,
+                                     (hipStream_t)stream));
+    } else
         HIPCHK(launch_encode_meta(ctx->geom, d_meta, d_var, d_acl, d_regions, d_payload_off, n,
                                   d_out, out_cap, d_out_off, d_status, (hipStream_t)stream));
     return HONU_OK;
@@ -268,7 +278,10 @@ int32_t honu_decode_parse(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
     if (rv == 2)
         HIPCHK(launch_decode_parse_grp(d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
                                        ctx->reg_inline, ctx->counts, (hipStream_t)stream));
-    else if (rv == 0 || rv == 3)
+    else if (rv == 0)
+        HIPCHK(launch_decode_parse_win(d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
+                                       ctx->reg_inline, ctx->counts, (hipStream_t)stream));
+    else if (rv == 3 || rv == 4)
         HIPCHK(launch_decode_parse_lane(d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
                                         ctx->reg_inline, ctx->counts, (hipStream_t)stream));
     else
@@ -292,7 +305,7 @@ int32_t honu_decode_tables(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n, honu
     uint64_t *tot = d_totals ? d_totals : ctx->totals;
     HIPCHK(launch_scan(ctx->counts, n, 3, ctx->offs, tot, ctx->partials, s));
     const int rv = ctx->geom.record_variant;
-    if (rv == 0 || rv == 2)
+    if (rv == 0 || rv == 2 || rv == 4)
         HIPCHK(launch_decode_fill_grp(d_rec, n, d_meta, d_info, ctx->scratch, ctx->reg_inline,
                                       ctx->counts, ctx->offs, d_acl, acl_cap, d_regions,
                                       regions_cap, d_data, data_cap, s));

@@ -868,6 +868,117 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_grp(
     }
 }
 
+
+// ------------------------------------------------------------------------
+// encode ACL entries (metadata.go:157-162, acls.go:26-39) into the gap the
+// lane encoder left at acl_pos[i]. With every entry present, output byte x of
+// the list is byte (x - P) % 18 of entry (x - P) / 18 encoded as
+// 01 | ClientID | Permissions, so each lane builds whole aligned 16-byte
+// output chunks from the (at most) two entries they straddle: coalesced entry
+// loads, one aligned store per chunk, byte stores only at the list's ends.
+// A list with nil entries is written serially by the group's lead lane.
+// ------------------------------------------------------------------------
+HONU_DEV void acl_enc_words(const honu_acl *e, uint32_t d[5]) {  // 18 encoded bytes
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(e);
+    const uint32_t e0 = w[0], e1 = w[1], e2 = w[2], e3 = w[3], e4 = w[4];
+    d[0] = 1u | (e0 << 8);
+    d[1] = (e0 >> 24) | (e1 << 8);
+    d[2] = (e1 >> 24) | (e2 << 8);
+    d[3] = (e2 >> 24) | (e3 << 8);
+    d[4] = (e3 >> 24) | ((e4 & 0xFF) << 8);
+}
+
+template <int G>
+__global__ __launch_bounds__(HONU_BLOCK) void k_encode_acl_grp(
+    const honu_meta *__restrict__ meta, const honu_acl *__restrict__ acl, uint64_t n,
+    uint8_t *__restrict__ out, const int32_t *__restrict__ status,
+    const uint64_t *__restrict__ acl_pos) {
+    const uint32_t r = threadIdx.x & (G - 1);
+    const uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G;
+    if (i >= n) return;
+    if (status[i] != HONU_OK) return;
+    const uint64_t na = meta[i].acl_count;
+    if (!na) return;
+    const honu_acl *A = acl + meta[i].acl_off;
+    const uint64_t P = acl_pos[i];
+    bool nil = false;
+    for (uint64_t j = r; j < na; j += G) nil |= A[j].present == 0;
+    if (grp_bits<G>(__ballot(nil)) != 0) {
+        if (r == 0) {  // 00 for a nil entry, else 01 | ClientID | Permissions
+            uint64_t p = P;
+            for (uint64_t j = 0; j < na; j++) {
+                if (A[j].present) {
+                    uint32_t d[5];
+                    acl_enc_words(A + j, d);
+                    for (int b = 0; b < 18; b++) out[p + b] = (uint8_t)(d[b >> 2] >> (8 * (b & 3)));
+                    p += 18;
+                } else {
+                    out[p++] = 0;
+                }
+            }
+        }
+        return;
+    }
+    const uint64_t E = P + 18 * na;          // end of the list
+    const uint64_t X0 = P & ~15ull;
+    const uint64_t nch = (E - X0 + 15) >> 4;
+    for (uint64_t c = r; c < nch; c += G) {
+        const uint64_t X = X0 + 16 * c;
+        const uint64_t lo = X > P ? X : P;   // first owned byte of the chunk
+        const uint64_t j0 = (lo - P) / 18;
+        uint32_t b[10];
+        acl_enc_words(A + j0, b);
+        b[5] = b[6] = b[7] = b[8] = b[9] = 0;
+        if (j0 + 1 < na) {  // entry j0 + 1 starts at byte 18 of b
+            uint32_t d[5];
+            acl_enc_words(A + j0 + 1, d);
+            b[4] = (b[4] & 0xFFFF) | (d[0] << 16);
+            b[5] = (d[0] >> 16) | (d[1] << 16);
+            b[6] = (d[1] >> 16) | (d[2] << 16);
+            b[7] = (d[2] >> 16) | (d[3] << 16);
+            b[8] = (d[3] >> 16) | (d[4] << 16);
+        }
+        // chunk byte k = b byte (X - P - 18 j0) + k; for the first chunk that
+        // offset is negative: shift b up instead and mask below P
+        const int64_t off = (int64_t)X - (int64_t)(P + 18 * j0);
+        uint32_t o[4];
+        if (off >= 0) {
+            const uint32_t q = (uint32_t)off >> 2, sh = (uint32_t)off & 3;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                uint32_t w0 = b[0], w1 = b[1];
+#pragma unroll
+                for (int t = 1; t <= 5; t++)
+                    if ((uint32_t)t == q) { w0 = b[t + k]; w1 = b[t + k + 1]; }
+                if (q == 0) { w0 = b[k]; w1 = b[k + 1]; }
+                o[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            }
+        } else {  // -15 <= off < 0: chunk byte k = b byte k + off
+            const uint32_t u = (uint32_t)(-off);  // 1..15
+            const uint32_t q = u >> 2, sh = u & 3;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                // word k of (b shifted up by u bytes) = bytes [4k - u, 4k - u + 4) of b
+                uint32_t hi = 0, lo2 = 0;
+#pragma unroll
+                for (int t = 0; t <= 3; t++) {
+                    if ((uint32_t)t == q) {
+                        hi = k - t >= 0 ? b[k - t] : 0;
+                        lo2 = k - t - 1 >= 0 ? b[k - t - 1] : 0;
+                    }
+                }
+                o[k] = sh ? __builtin_amdgcn_alignbyte(hi, lo2, 4 - sh) : hi;
+            }
+        }
+        if (X >= P && X + 16 <= E) {
+            *reinterpret_cast<u32x4 *>(out + X) = u32x4{o[0], o[1], o[2], o[3]};
+        } else {
+            for (uint32_t k = 0; k < 16; k++)
+                if (X + k >= P && X + k < E) out[X + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
+        }
+    }
+}
+
 #undef OFF
 
 static dim3 grp_grid(uint64_t n) {
@@ -891,6 +1002,15 @@ hipError_t launch_encode_meta_grp(const honu_meta *meta, const uint8_t *var, con
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_encode_meta_grp<GRP>, grp_grid(n), dim3(HONU_BLOCK), 0, s, meta, var, acl,
                        reg, payload_off, n, out, out_cap, out_off, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uint64_t n,
+                                 uint8_t *out, const int32_t *status, const uint64_t *acl_pos,
+                                 hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_encode_acl_grp<GRP>, grp_grid(n), dim3(HONU_BLOCK), 0, s, meta, acl, n,
+                       out, status, acl_pos);
     return hipGetLastError();
 }
 

@@ -291,6 +291,15 @@ struct LaneWriter {
     HONU_DEV void finish() {
         if (f > first) store_bytes(first, f);
     }
+    // absolute position of the next byte
+    HONU_DEV uint64_t pos() const { return cpos + f; }
+    // continue at `to` (>= pos()); bytes in between are left to another writer
+    HONU_DEV void jump(uint64_t to) {
+        finish();
+        cpos = to & ~15ull;
+        f = first = (uint32_t)(to & 15);
+        a0 = a1 = 0;
+    }
 };
 
 }  // namespace honu

@@ -384,11 +384,16 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_sizes_lane(
 // ------------------------------------------------------------------------
 HONU_DEV uint64_t ld64(const uint8_t *p) { return *reinterpret_cast<const uint64_t *>(p); }
 
+// SKIP_ACL: leave the ACL entries to k_encode_acl_grp (grp.hip): write the
+// fields up to uvarint(len ACL), record that position in acl_out[i], and
+// resume at end - (bytes after the list), computed from the row and regions.
+template <bool SKIP_ACL>
 __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
     const honu_meta *__restrict__ meta, const uint8_t *__restrict__ var,
     const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
     const uint64_t *__restrict__ payload_off, uint64_t n, uint8_t *__restrict__ out,
-    uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status) {
+    uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status,
+    uint64_t *__restrict__ acl_out) {
     const uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x;
     if (i >= n) return;
     if (status[i] != HONU_OK) return;
@@ -452,6 +457,25 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
     W.byte(m.permissions);                                          // :145
     const uint64_t na = m.acl_count, ao = m.acl_off;
     W.uv(na);                                                       // :151
+    const uint64_t nr = m.regions_count, ro = m.regions_off;
+    if constexpr (SKIP_ACL) {
+        acl_out[i] = W.pos();
+        uint64_t sfx = uvarint_len(nr) + 3 + 1 + uvarint_len(zigzag(m.created)) +
+                       uvarint_len(zigzag(m.modified));
+        for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
+            uint32_t r8[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? reg[ro + k0 + j] : 0;
+#pragma unroll
+            for (int j = 0; j < 8; j++) sfx += k0 + j < nr ? uvarint_len(r8[j]) : 0;
+        }
+        if (pr & HONU_HAS_PUBLISHER) sfx += 32 + frame_len(m.ip_address.len) + frame_len(m.user_agent.len);
+        if (pr & HONU_HAS_ENCRYPTION)
+            sfx += frame_len(m.public_key_id.len) + frame_len(m.encryption_key.len) +
+                   frame_len(m.hmac_secret.len) + frame_len(m.signature.len) + 3;
+        if (pr & HONU_HAS_COMPRESSION) sfx += 1 + uvarint_len(zigzag(m.compression_level));
+        W.jump(end - sfx);
+    } else {
     for (uint64_t k0 = 0; k0 < na; k0 += 8) {                       // :157-162, acls.go:26-39
         uint32_t e[8][5];                                            // 8 entries ahead
 #pragma unroll
@@ -475,7 +499,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
             }
         }
     }
-    const uint64_t nr = m.regions_count, ro = m.regions_off;
+    }
     W.uv(nr);                                                       // :164, region.go:137-152
     for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
         uint32_t r8[8];
@@ -561,10 +585,14 @@ namespace honu {
 hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
                                    const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
                                    uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
-                                   int32_t *status, hipStream_t s) {
+                                   int32_t *status, uint64_t *acl_out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_encode_meta_lane, lane_grid(n), dim3(HONU_BLOCK), 0, s, meta, var, acl,
-                       reg, payload_off, n, out, out_cap, out_off, status);
+    if (acl_out)
+        hipLaunchKernelGGL(k_encode_meta_lane<true>, lane_grid(n), dim3(HONU_BLOCK), 0, s, meta,
+                           var, acl, reg, payload_off, n, out, out_cap, out_off, status, acl_out);
+    else
+        hipLaunchKernelGGL(k_encode_meta_lane<false>, lane_grid(n), dim3(HONU_BLOCK), 0, s, meta,
+                           var, acl, reg, payload_off, n, out, out_cap, out_off, status, acl_out);
     return hipGetLastError();
 }
 }  // namespace honu

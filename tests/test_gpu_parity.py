@@ -20,10 +20,12 @@ from honu_amd.metadata import META_DTYPE, normalize, pack_batch, unpack_row  # n
 from honu_amd.workload import gen_host_batch, gen_meta  # noqa: E402
 
 
-@pytest.fixture(scope="module", params=[0, 1, 2, 3], ids=["auto", "wave", "group", "lane"])
+@pytest.fixture(scope="module", params=[0, 1, 2, 3, 4],
+                ids=["auto", "wave", "group", "lane", "lane+group"])
 def codec(request):
-    """Every metadata-kernel variant: auto (the default per-kernel choice), one
-    record per wave, per group of 16 lanes, per lane."""
+    """Every metadata-kernel variant: auto (the default per-kernel choice: split
+    lane/group encode, windowed lane parse), one record per wave, per group of
+    16 lanes, per lane, and lane encode/parse with the group size pass/fill."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     c = hobj.Codec(0, 1 << 16)
