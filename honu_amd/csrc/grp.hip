@@ -795,10 +795,12 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_grp(
     const uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G;
     if (i >= n) return;
     honu_record_info *inf = info + i;
+    // independent loads first (one round trip)
     const int32_t mst = inf->meta_status;
+    const uint64_t na = counts[3 * i], nr = counts[3 * i + 1];
+    const uint64_t ao = offs[3 * i], ro = offs[3 * i + 1];
+    const DecodeScratch sc = scratch[i];
     if (mst == HONU_OK) {
-        const uint64_t na = counts[3 * i], nr = counts[3 * i + 1];
-        const uint64_t ao = offs[3 * i], ro = offs[3 * i + 1];
         if (r == 0) {
             if (na) meta[i].acl_off = ao;
             if (nr) meta[i].regions_off = ro;
@@ -806,21 +808,34 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_grp(
         if (ao + na > acl_cap || ro + nr > reg_cap) {
             if (r == 0) inf->meta_status = HONU_ERR_CAPACITY;
         } else if (na + nr) {
-            const DecodeScratch sc = scratch[i];
             const uint64_t end = sc.rec_end;
             const uint64_t ap = sc.acl_pos & GRP_POS_MASK;
             if (na && (sc.acl_pos & GRP_ACL_FAST)) {
-                for (uint64_t j = r; j < na; j += G) {
-                    const uint64_t q = ap + 18 * j;
-                    uint64_t lo, hi;
-                    lane_fetch16(rec, q + 1, end, lo, hi);
-                    const uint32_t pm = rec[q + 17];
-                    uint32_t *e = reinterpret_cast<uint32_t *>(acl + ao + j);
-                    e[0] = (uint32_t)lo;
-                    e[1] = (uint32_t)(lo >> 32);
-                    e[2] = (uint32_t)hi;
-                    e[3] = (uint32_t)(hi >> 32);
-                    e[4] = pm | (1u << 8);
+                constexpr int K = 4;  // entries per lane loaded before any store
+                for (uint64_t j0 = r; j0 < na; j0 += (uint64_t)G * K) {
+                    uint64_t lo[K], hi[K];
+                    uint32_t pm[K];
+#pragma unroll
+                    for (int k = 0; k < K; k++) {
+                        const uint64_t j = j0 + (uint64_t)G * k;
+                        if (j < na) {
+                            const uint64_t q = ap + 18 * j;
+                            lane_fetch16(rec, q + 1, end, lo[k], hi[k]);
+                            pm[k] = rec[q + 17];
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < K; k++) {
+                        const uint64_t j = j0 + (uint64_t)G * k;
+                        if (j < na) {
+                            uint32_t *e = reinterpret_cast<uint32_t *>(acl + ao + j);
+                            e[0] = (uint32_t)lo[k];
+                            e[1] = (uint32_t)(lo[k] >> 32);
+                            e[2] = (uint32_t)hi[k];
+                            e[3] = (uint32_t)(hi[k] >> 32);
+                            e[4] = pm[k] | (1u << 8);
+                        }
+                    }
                 }
             } else if (na && r == 0) {  // nil entries: walk (validated by the parse)
                 uint64_t p = ap;
@@ -878,14 +893,37 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_grp(
 // loads, one aligned store per chunk, byte stores only at the list's ends.
 // A list with nil entries is written serially by the group's lead lane.
 // ------------------------------------------------------------------------
-HONU_DEV void acl_enc_words(const honu_acl *e, uint32_t d[5]) {  // 18 encoded bytes
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(e);
-    const uint32_t e0 = w[0], e1 = w[1], e2 = w[2], e3 = w[3], e4 = w[4];
-    d[0] = 1u | (e0 << 8);
-    d[1] = (e0 >> 24) | (e1 << 8);
-    d[2] = (e1 >> 24) | (e2 << 8);
-    d[3] = (e2 >> 24) | (e3 << 8);
-    d[4] = (e3 >> 24) | ((e4 & 0xFF) << 8);
+// 16 output bytes at absolute X >= P of the list at P (every entry present)
+HONU_DEV u32x4 acl_chunk(const honu_acl *A, uint64_t na, uint64_t P, uint64_t X) {
+    const uint64_t j0 = (X - P) / 18;
+    uint32_t b[10];
+    acl_enc_words(A + j0, b);
+    b[5] = b[6] = b[7] = b[8] = b[9] = 0;
+    if (j0 + 1 < na) {  // entry j0 + 1 starts at byte 18 of b
+        uint32_t d[5];
+        acl_enc_words(A + j0 + 1, d);
+        b[4] = (b[4] & 0xFFFF) | (d[0] << 16);
+        b[5] = (d[0] >> 16) | (d[1] << 16);
+        b[6] = (d[1] >> 16) | (d[2] << 16);
+        b[7] = (d[2] >> 16) | (d[3] << 16);
+        b[8] = (d[3] >> 16) | (d[4] << 16);
+    }
+    // chunk byte k = byte (X - P - 18 j0) + k of b (X >= P)
+    const uint32_t off = (uint32_t)(X - (P + 18 * j0));
+    const uint32_t q = off >> 2, sh = off & 3;
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        uint32_t w0 = b[k], w1 = b[k + 1];
+#pragma unroll
+        for (int t = 1; t <= 4; t++)
+            if ((uint32_t)t == q) {
+                w0 = b[t + k];
+                w1 = b[t + k + 1];
+            }
+        o[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    }
+    return u32x4{o[0], o[1], o[2], o[3]};
 }
 
 template <int G>
@@ -896,85 +934,43 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_acl_grp(
     const uint32_t r = threadIdx.x & (G - 1);
     const uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G;
     if (i >= n) return;
-    if (status[i] != HONU_OK) return;
-    const uint64_t na = meta[i].acl_count;
-    if (!na) return;
-    const honu_acl *A = acl + meta[i].acl_off;
-    const uint64_t P = acl_pos[i];
-    bool nil = false;
-    for (uint64_t j = r; j < na; j += G) nil |= A[j].present == 0;
-    if (grp_bits<G>(__ballot(nil)) != 0) {
-        if (r == 0) {  // 00 for a nil entry, else 01 | ClientID | Permissions
-            uint64_t p = P;
-            for (uint64_t j = 0; j < na; j++) {
-                if (A[j].present) {
-                    uint32_t d[5];
-                    acl_enc_words(A + j, d);
-                    for (int b = 0; b < 18; b++) out[p + b] = (uint8_t)(d[b >> 2] >> (8 * (b & 3)));
-                    p += 18;
-                } else {
-                    out[p++] = 0;
-                }
+    // independent loads first: one round trip before the entries
+    const int32_t sti = status[i];
+    const uint64_t na = meta[i].acl_count, ao = meta[i].acl_off, pos = acl_pos[i];
+    if (sti != HONU_OK || !na) return;
+    const honu_acl *A = acl + ao;
+    const uint64_t P = pos & ~ACL_ALL_PRESENT;
+    if (pos & ACL_ALL_PRESENT) {  // whole chunks [ceil16(P), floor16(E))
+        const uint64_t X0 = (P + 15) & ~15ull, X1 = (P + 18 * na) & ~15ull;
+        if (X1 <= X0) return;
+        const uint64_t nch = (X1 - X0) >> 4;
+        constexpr int K = 2;  // chunks per lane computed before any store
+        for (uint64_t c0 = r; c0 < nch; c0 += (uint64_t)G * K) {
+            u32x4 v[K];
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const uint64_t c = c0 + (uint64_t)G * k;
+                if (c < nch) v[k] = acl_chunk(A, na, P, X0 + 16 * c);
+            }
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const uint64_t c = c0 + (uint64_t)G * k;
+                if (c < nch) *reinterpret_cast<u32x4 *>(out + X0 + 16 * c) = v[k];
             }
         }
         return;
     }
-    const uint64_t E = P + 18 * na;          // end of the list
-    const uint64_t X0 = P & ~15ull;
-    const uint64_t nch = (E - X0 + 15) >> 4;
-    for (uint64_t c = r; c < nch; c += G) {
-        const uint64_t X = X0 + 16 * c;
-        const uint64_t lo = X > P ? X : P;   // first owned byte of the chunk
-        const uint64_t j0 = (lo - P) / 18;
-        uint32_t b[10];
-        acl_enc_words(A + j0, b);
-        b[5] = b[6] = b[7] = b[8] = b[9] = 0;
-        if (j0 + 1 < na) {  // entry j0 + 1 starts at byte 18 of b
-            uint32_t d[5];
-            acl_enc_words(A + j0 + 1, d);
-            b[4] = (b[4] & 0xFFFF) | (d[0] << 16);
-            b[5] = (d[0] >> 16) | (d[1] << 16);
-            b[6] = (d[1] >> 16) | (d[2] << 16);
-            b[7] = (d[2] >> 16) | (d[3] << 16);
-            b[8] = (d[3] >> 16) | (d[4] << 16);
-        }
-        // chunk byte k = b byte (X - P - 18 j0) + k; for the first chunk that
-        // offset is negative: shift b up instead and mask below P
-        const int64_t off = (int64_t)X - (int64_t)(P + 18 * j0);
-        uint32_t o[4];
-        if (off >= 0) {
-            const uint32_t q = (uint32_t)off >> 2, sh = (uint32_t)off & 3;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                uint32_t w0 = b[0], w1 = b[1];
-#pragma unroll
-                for (int t = 1; t <= 5; t++)
-                    if ((uint32_t)t == q) { w0 = b[t + k]; w1 = b[t + k + 1]; }
-                if (q == 0) { w0 = b[k]; w1 = b[k + 1]; }
-                o[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    if (r == 0) {  // nil entries: 00 for a nil entry, else 01 | ClientID | Permissions
+        uint64_t p = P;
+        for (uint64_t j = 0; j < na; j++) {
+            if (A[j].present) {
+                uint32_t d[5];
+                acl_enc_words(A + j, d);
+                for (int b = 0; b < 18; b++) out[p + b] = (uint8_t)(d[b >> 2] >> (8 * (b & 3)));
+                p += 18;
+            } else {
+                out[p++] = 0;
             }
-        } else {  // -15 <= off < 0: chunk byte k = b byte k + off
-            const uint32_t u = (uint32_t)(-off);  // 1..15
-            const uint32_t q = u >> 2, sh = u & 3;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                // word k of (b shifted up by u bytes) = bytes [4k - u, 4k - u + 4) of b
-                uint32_t hi = 0, lo2 = 0;
-#pragma unroll
-                for (int t = 0; t <= 3; t++) {
-                    if ((uint32_t)t == q) {
-                        hi = k - t >= 0 ? b[k - t] : 0;
-                        lo2 = k - t - 1 >= 0 ? b[k - t - 1] : 0;
-                    }
-                }
-                o[k] = sh ? __builtin_amdgcn_alignbyte(hi, lo2, 4 - sh) : hi;
-            }
-        }
-        if (X >= P && X + 16 <= E) {
-            *reinterpret_cast<u32x4 *>(out + X) = u32x4{o[0], o[1], o[2], o[3]};
-        } else {
-            for (uint32_t k = 0; k < 16; k++)
-                if (X + k >= P && X + k < E) out[X + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
         }
     }
 }

@@ -26,6 +26,22 @@ struct DecodeScratch {
 #define GRP_ACL_FAST (1ull << 63)    // acl_pos: every entry present, entry j at acl_pos + 18 j
 #define GRP_REG_INLINE (1ull << 62)  // regions_pos: region ids in reg_inline[8 i ..]
 #define GRP_POS_MASK (~(GRP_ACL_FAST | GRP_REG_INLINE))
+// Flag on the lane encoder's ACL list position: every entry present, and the
+// list's partial end chunks are already written (the group kernel stores the
+// whole chunks in between).
+#define ACL_ALL_PRESENT (1ull << 63)
+
+// 01 | ClientID | Permissions, the 18 encoded bytes of a present
+// *AccessControl (acls.go:26-39), as 4.5 little-endian words.
+HONU_DEV void acl_enc_words(const honu_acl *e, uint32_t d[5]) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(e);
+    const uint32_t e0 = w[0], e1 = w[1], e2 = w[2], e3 = w[3], e4 = w[4];
+    d[0] = 1u | (e0 << 8);
+    d[1] = (e0 >> 24) | (e1 << 8);
+    d[2] = (e1 >> 24) | (e2 << 8);
+    d[3] = (e2 >> 24) | (e3 << 8);
+    d[4] = (e3 >> 24) | ((e4 & 0xFF) << 8);
+}
 
 struct LaunchGeom {
     int num_cu;

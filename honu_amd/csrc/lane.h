@@ -216,9 +216,26 @@ struct LaneWriter {
         f = first = (uint32_t)(pos & 15);
         a0 = a1 = 0;
     }
+    // bytes [from, to) of the chunk with the widest aligned stores that fit
+    // (at most 1 + 1 + 1 + 1 + 1 + 1 stores instead of one per byte)
     HONU_DEV void store_bytes(uint32_t from, uint32_t to) {
-        for (uint32_t j = from; j < to; j++)
-            out[cpos + j] = (uint8_t)((j < 8 ? a0 >> (8 * j) : a1 >> (8 * (j - 8))) & 0xFF);
+        uint8_t *p = out + cpos;
+        uint32_t j = from;
+        auto bytes_at = [&](uint32_t k, uint32_t n) -> uint64_t {  // n <= 8, k + n <= 16
+            uint64_t v = k < 8 ? (a0 >> (8 * k)) | (k ? a1 << (64 - 8 * k) : 0) : a1 >> (8 * (k - 8));
+            return n == 8 ? v : v & ((1ull << (8 * n)) - 1);
+        };
+        if ((j & 1) && j < to) { p[j] = (uint8_t)bytes_at(j, 1); j += 1; }
+        if ((j & 2) && j + 2 <= to) { *reinterpret_cast<uint16_t *>(p + j) = (uint16_t)bytes_at(j, 2); j += 2; }
+        if ((j & 4) && j + 4 <= to) { *reinterpret_cast<uint32_t *>(p + j) = (uint32_t)bytes_at(j, 4); j += 4; }
+        if (j == 0 && to == 16) {
+            *reinterpret_cast<u32x4 *>(p) = u32x4{(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32)};
+            return;
+        }
+        if (j + 8 <= to) { *reinterpret_cast<uint64_t *>(p + j) = bytes_at(j, 8); j += 8; }
+        if (j + 4 <= to) { *reinterpret_cast<uint32_t *>(p + j) = (uint32_t)bytes_at(j, 4); j += 4; }
+        if (j + 2 <= to) { *reinterpret_cast<uint16_t *>(p + j) = (uint16_t)bytes_at(j, 2); j += 2; }
+        if (j < to) p[j] = (uint8_t)bytes_at(j, 1);
     }
     HONU_DEV void flush() {
         if (first == 0)

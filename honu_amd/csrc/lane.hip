@@ -459,7 +459,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
     W.uv(na);                                                       // :151
     const uint64_t nr = m.regions_count, ro = m.regions_off;
     if constexpr (SKIP_ACL) {
-        acl_out[i] = W.pos();
+        const uint64_t P = W.pos();
         uint64_t sfx = uvarint_len(nr) + 3 + 1 + uvarint_len(zigzag(m.created)) +
                        uvarint_len(zigzag(m.modified));
         for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
@@ -474,7 +474,38 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
             sfx += frame_len(m.public_key_id.len) + frame_len(m.encryption_key.len) +
                    frame_len(m.hmac_secret.len) + frame_len(m.signature.len) + 3;
         if (pr & HONU_HAS_COMPRESSION) sfx += 1 + uvarint_len(zigzag(m.compression_level));
-        W.jump(end - sfx);
+        const uint64_t E = end - sfx;  // the list is [P, E)
+        if (na && E - P == 18 * na) {
+            // every entry present (a nil entry is 1 byte): this lane writes the
+            // list's bytes in the partial 16-byte chunks at both ends, so the
+            // group kernel stores whole aligned chunks only
+            acl_out[i] = P | ACL_ALL_PRESENT;
+            const uint64_t hend = ((P + 15) & ~15ull) < E ? ((P + 15) & ~15ull) : E;
+            const uint64_t T = (E & ~15ull) > hend ? (E & ~15ull) : hend;
+            for (uint64_t x = P; x < E;) {
+                if (x == hend && x < T) {
+                    W.jump(T);
+                    x = T;
+                    continue;
+                }
+                const uint64_t j = (x - P) / 18;
+                uint32_t d[5];
+                acl_enc_words(acl + ao + j, d);
+                const uint64_t lo = ((uint64_t)d[1] << 32) | d[0], hi = ((uint64_t)d[3] << 32) | d[2];
+                const uint64_t stop = P + 18 * (j + 1) < (x < hend ? hend : E) ? P + 18 * (j + 1)
+                                                                             : (x < hend ? hend : E);
+                for (; x < stop; x++) {
+                    const uint32_t k = (uint32_t)(x - P - 18 * j);
+                    const uint32_t bv = k < 8 ? (uint32_t)(lo >> (8 * k))
+                                              : k < 16 ? (uint32_t)(hi >> (8 * (k - 8)))
+                                                       : d[4] >> (8 * (k - 16));
+                    W.byte(bv);
+                }
+            }
+        } else {
+            acl_out[i] = P;
+            W.jump(E);
+        }
     } else {
     for (uint64_t k0 = 0; k0 < na; k0 += 8) {                       // :157-162, acls.go:26-39
         uint32_t e[8][5];                                            // 8 entries ahead
