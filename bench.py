@@ -60,6 +60,10 @@ def parse_args():
     p.add_argument("--serial", action="store_true", help="one stream, no metadata/copy overlap")
     p.add_argument("--meta-blocks", type=int, default=2,
                    help="workgroups per CU for the per-record kernels (0 = library default)")
+    p.add_argument("--lane-blocks", type=int, default=-1,
+                   help="workgroups per CU for the lane/group metadata kernels while copies run "
+                        "beside them (0 = no cap; -1 = auto: 2 when records average > 64 KiB, "
+                        "where the copies dominate, else no cap)")
     p.add_argument("--copy-prio", type=int, default=1, help="copy stream gets high priority")
     return p.parse_args()
 
@@ -143,11 +147,18 @@ class Bench:
         nslots = 1 if args.serial else 2
         self.slots = [Slot(self.dev, C, self.out_cap, self.acl_cap, self.reg_cap, self.data_cap)
                       for _ in range(nslots)]
-        if args.meta_blocks and not args.serial:
-            ncu = torch.cuda.get_device_properties(self.dev).multi_processor_count
+        ncu = torch.cuda.get_device_properties(self.dev).multi_processor_count
+        lane_blocks = args.lane_blocks
+        if lane_blocks < 0:
+            lane_blocks = 2 if self.total_rec_bytes / N > 65536 else 0
+        self.lane_blocks = 0 if args.serial else lane_blocks
+        if not args.serial:
             for sl in self.slots:
-                _lib.check(self.lib.honu_ctx_set_param(sl.codec.ctx, b"record_blocks",
-                                                       args.meta_blocks * ncu), "param")
+                if args.meta_blocks:
+                    _lib.check(self.lib.honu_ctx_set_param(sl.codec.ctx, b"record_blocks",
+                                                           args.meta_blocks * ncu), "param")
+                _lib.check(self.lib.honu_ctx_set_param(sl.codec.ctx, b"lane_blocks",
+                                                       self.lane_blocks * ncu), "param")
         self.sm = torch.cuda.Stream(self.dev)  # metadata kernels
         # payload copies: the bandwidth-bound critical path, dispatched first
         self.sc = (torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio else 0)
@@ -469,6 +480,7 @@ def main():
             "parallelism": f"dp{world} (records sharded, no data-path collective)",
             "streams": 1 if args.serial else 2,
             "meta_blocks_per_cu": 8 if (args.serial or not args.meta_blocks) else args.meta_blocks,
+            "lane_blocks_per_cu": bench.lane_blocks or None,
         },
         "records_per_s": total_records / step_s,
         "roofline": {

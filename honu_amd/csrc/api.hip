@@ -106,6 +106,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->max_n = max_records ? max_records : 1;
     c->geom.num_cu = prop.multiProcessorCount;
     c->geom.per_record_blocks = env_int("HONU_RECORD_BLOCKS", prop.multiProcessorCount * 8);
+    c->geom.lane_blocks = env_int("HONU_LANE_BLOCKS", 0);
     c->geom.copy_blocks = env_int("HONU_COPY_BLOCKS", prop.multiProcessorCount * 2);
     c->geom.copy_variant = env_int("HONU_COPY_VARIANT", 0);
     c->geom.record_variant = env_int("HONU_RECORD_VARIANT", 0);
@@ -151,6 +152,7 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
     if (!ctx || !name) return arg_fail("ctx/name");
     if (!strcmp(name, "copy_blocks") && value > 0) ctx->geom.copy_blocks = (int)value;
     else if (!strcmp(name, "record_blocks") && value > 0) ctx->geom.per_record_blocks = (int)value;
+    else if (!strcmp(name, "lane_blocks") && value >= 0) ctx->geom.lane_blocks = (int)value;
     else if (!strcmp(name, "copy_variant") && value >= 0) ctx->geom.copy_variant = (int)value;
     else if (!strcmp(name, "record_variant") && value >= 0) ctx->geom.record_variant = (int)value;
     else return arg_fail(name);
@@ -171,10 +173,12 @@ int32_t honu_encode_sizes(honu_ctx *ctx, const honu_meta *d_meta, uint64_t var_l
     const int rv = ctx->geom.record_variant;
     if (rv == 0 || rv == 2 || rv == 4)
         HIPCHK(launch_encode_sizes_grp(d_meta, var_len, d_acl, acl_len, d_regions, regions_len,
-                                       d_payload_off, n, d_sizes, d_status, (hipStream_t)stream));
+                                       d_payload_off, n, d_sizes, d_status, ctx->geom.lane_blocks,
+                                       (hipStream_t)stream));
     else if (rv == 3)
         HIPCHK(launch_encode_sizes_lane(d_meta, var_len, d_acl, acl_len, d_regions, regions_len,
-                                        d_payload_off, n, d_sizes, d_status, (hipStream_t)stream));
+                                        d_payload_off, n, d_sizes, d_status, ctx->geom.lane_blocks,
+                                       (hipStream_t)stream));
     else
         HIPCHK(launch_encode_sizes(ctx->geom, d_meta, var_len, d_acl, acl_len, d_regions,
                                    regions_len, d_payload_off, n, d_sizes, d_status,
@@ -204,18 +208,19 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
     const int rv = ctx->geom.record_variant;
     if (rv == 2)
         HIPCHK(launch_encode_meta_grp(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
-                                      out_cap, d_out_off, d_status, (hipStream_t)stream));
+                                      out_cap, d_out_off, d_status, ctx->geom.lane_blocks,
+                                       (hipStream_t)stream));
     else if (rv == 3 || rv == 4)
         HIPCHK(launch_encode_meta_lane(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
-                                       out_cap, d_out_off, d_status, nullptr,
+                                       out_cap, d_out_off, d_status, nullptr, ctx->geom.lane_blocks,
                                        (hipStream_t)stream));
     else if (rv == 0) {
         if (n > ctx->max_n) return HONU_E_WORKSPACE;
         HIPCHK(launch_encode_meta_lane(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
-                                       out_cap, d_out_off, d_status, ctx->enc_acl,
+                                       out_cap, d_out_off, d_status, ctx->enc_acl, ctx->geom.lane_blocks,
                                        (hipStream_t)stream));
-        HIPCHK(launch_encode_acl_grp(d_meta, d_acl, n, d_out, d_status, ctx->enc_acl,
-                                     (hipStream_t)stream));
+        HIPCHK(launch_encode_acl_grp(d_meta, d_acl, n, d_out, d_status, ctx->enc_acl, ctx->geom.lane_blocks,
+                                       (hipStream_t)stream));
     } else
         HIPCHK(launch_encode_meta(ctx->geom, d_meta, d_var, d_acl, d_regions, d_payload_off, n,
                                   d_out, out_cap, d_out_off, d_status, (hipStream_t)stream));
@@ -277,13 +282,16 @@ int32_t honu_decode_parse(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
     const int rv = ctx->geom.record_variant;
     if (rv == 2)
         HIPCHK(launch_decode_parse_grp(d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
-                                       ctx->reg_inline, ctx->counts, (hipStream_t)stream));
+                                       ctx->reg_inline, ctx->counts, ctx->geom.lane_blocks,
+                                       (hipStream_t)stream));
     else if (rv == 0)
         HIPCHK(launch_decode_parse_win(d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
-                                       ctx->reg_inline, ctx->counts, (hipStream_t)stream));
+                                       ctx->reg_inline, ctx->counts, ctx->geom.lane_blocks,
+                                       (hipStream_t)stream));
     else if (rv == 3 || rv == 4)
         HIPCHK(launch_decode_parse_lane(d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
-                                        ctx->reg_inline, ctx->counts, (hipStream_t)stream));
+                                        ctx->reg_inline, ctx->counts, ctx->geom.lane_blocks,
+                                       (hipStream_t)stream));
     else
         HIPCHK(launch_decode_parse(ctx->geom, d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
                                    ctx->counts, (hipStream_t)stream));
@@ -308,11 +316,11 @@ int32_t honu_decode_tables(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n, honu
     if (rv == 0 || rv == 2 || rv == 4)
         HIPCHK(launch_decode_fill_grp(d_rec, n, d_meta, d_info, ctx->scratch, ctx->reg_inline,
                                       ctx->counts, ctx->offs, d_acl, acl_cap, d_regions,
-                                      regions_cap, d_data, data_cap, s));
+                                      regions_cap, d_data, data_cap, ctx->geom.lane_blocks, s));
     else if (rv == 3)
         HIPCHK(launch_decode_fill_lane(d_rec, n, d_meta, d_info, ctx->scratch, ctx->counts,
                                        ctx->offs, d_acl, acl_cap, d_regions, regions_cap, d_data,
-                                       data_cap, s));
+                                       data_cap, ctx->geom.lane_blocks, s));
     else
         HIPCHK(launch_decode_fill(ctx->geom, d_rec, n, d_meta, d_info, ctx->scratch, ctx->counts,
                                   ctx->offs, tot, d_acl, acl_cap, d_regions, regions_cap, d_data,

@@ -320,15 +320,11 @@ template <int G> HONU_DEV void grp_stage_row(uint8_t *row, const honu_meta *src,
 // encode: header + Metadata tail (object.go:24-45)
 // ------------------------------------------------------------------------
 template <int G>
-__global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_grp(
-    const honu_meta *__restrict__ meta, const uint8_t *__restrict__ var,
+HONU_DEV void k_encode_meta_grp_one(uint64_t i, uint8_t *smem, const honu_meta *__restrict__ meta, const uint8_t *__restrict__ var,
     const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
     const uint64_t *__restrict__ payload_off, uint64_t n, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[GRECS * GPER];
     const uint32_t r = threadIdx.x & (G - 1);
-    const uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G;
-    if (i >= n) return;
     if (status[i] != HONU_OK) return;
     const uint64_t beg = out_off[i], end = out_off[i + 1];
     if (end > out_cap) {
@@ -376,6 +372,18 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_grp(
     }
 }
 
+template <int G>
+__global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_grp(
+    const honu_meta *__restrict__ meta, const uint8_t *__restrict__ var,
+    const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
+    const uint64_t *__restrict__ payload_off, uint64_t n, uint8_t *__restrict__ out,
+    uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[GRECS * GPER];
+    for (uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G; i < n;
+         i += (uint64_t)gridDim.x * (HONU_BLOCK / G))
+        k_encode_meta_grp_one<G>(i, smem, meta, var, acl, reg, payload_off, n, out, out_cap, out_off, status);
+}
+
 // ------------------------------------------------------------------------
 // encode size pass (object.go:24-45 / App. A), row image staged in LDS
 // ------------------------------------------------------------------------
@@ -385,15 +393,11 @@ HONU_DEV bool gspan_in(uint64_t off, uint64_t len, uint64_t var_len) {
 HONU_DEV uint64_t gframe_len(uint64_t len) { return uvarint_len(len) + len; }
 
 template <int G>
-__global__ __launch_bounds__(HONU_BLOCK) void k_encode_sizes_grp(
-    const honu_meta *__restrict__ meta, uint64_t var_len, const honu_acl *__restrict__ acl,
+HONU_DEV void k_encode_sizes_grp_one(uint64_t i, uint8_t *smem, const honu_meta *__restrict__ meta, uint64_t var_len, const honu_acl *__restrict__ acl,
     uint64_t acl_len, const uint32_t *__restrict__ reg, uint64_t reg_len,
     const uint64_t *__restrict__ payload_off, uint64_t n, uint64_t *__restrict__ sizes,
     int32_t *__restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[GRECS * (GROW + 16)];
     const uint32_t r = threadIdx.x & (G - 1);
-    const uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G;
-    if (i >= n) return;
     uint8_t *row = smem + (threadIdx.x / G) * (GROW + 16);
     grp_stage_row<G>(row, meta + i, r);
     wave_sync();
@@ -452,6 +456,18 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_sizes_grp(
         sizes[i] = size;
         if (status) status[i] = stc;
     }
+}
+
+template <int G>
+__global__ __launch_bounds__(HONU_BLOCK) void k_encode_sizes_grp(
+    const honu_meta *__restrict__ meta, uint64_t var_len, const honu_acl *__restrict__ acl,
+    uint64_t acl_len, const uint32_t *__restrict__ reg, uint64_t reg_len,
+    const uint64_t *__restrict__ payload_off, uint64_t n, uint64_t *__restrict__ sizes,
+    int32_t *__restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[GRECS * (GROW + 16)];
+    for (uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G; i < n;
+         i += (uint64_t)gridDim.x * (HONU_BLOCK / G))
+        k_encode_sizes_grp_one<G>(i, smem, meta, var_len, acl, acl_len, reg, reg_len, payload_off, n, sizes, status);
 }
 
 // ------------------------------------------------------------------------
@@ -680,15 +696,11 @@ template <int G> HONU_DEV void grp_zero_row(uint8_t *row, uint32_t r) {
 }
 
 template <int G>
-__global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_grp(
-    const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
+HONU_DEV void k_decode_parse_grp_one(uint64_t i, uint8_t *smem, const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
     honu_meta *__restrict__ meta, honu_record_info *__restrict__ info,
     DecodeScratch *__restrict__ scratch, uint32_t *__restrict__ reg_inline,
     uint64_t *__restrict__ counts) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[GRECS * GPER];
     const uint32_t r = threadIdx.x & (G - 1);
-    const uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G;
-    if (i >= n) return;
     uint8_t *row = smem + (threadIdx.x / G) * GPER;
     uint8_t *stage = row + GROW;
     const uint64_t beg = rec_off[i], end = rec_off[i + 1];
@@ -781,19 +793,28 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_grp(
     if (r < 8 && r < nreg) reg_inline[8 * i + r] = myreg;
 }
 
+template <int G>
+__global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_grp(
+    const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
+    honu_meta *__restrict__ meta, honu_record_info *__restrict__ info,
+    DecodeScratch *__restrict__ scratch, uint32_t *__restrict__ reg_inline,
+    uint64_t *__restrict__ counts) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[GRECS * GPER];
+    for (uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G; i < n;
+         i += (uint64_t)gridDim.x * (HONU_BLOCK / G))
+        k_decode_parse_grp_one<G>(i, smem, rec, rec_off, n, meta, info, scratch, reg_inline, counts);
+}
+
 // ------------------------------------------------------------------------
 // decode fill: ACL/region tables and offsets (after the count scans)
 // ------------------------------------------------------------------------
 template <int G>
-__global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_grp(
-    const uint8_t *__restrict__ rec, uint64_t n, honu_meta *__restrict__ meta,
+HONU_DEV void k_decode_fill_grp_one(uint64_t i, const uint8_t *__restrict__ rec, uint64_t n, honu_meta *__restrict__ meta,
     honu_record_info *__restrict__ info, const DecodeScratch *__restrict__ scratch,
     const uint32_t *__restrict__ reg_inline, const uint64_t *__restrict__ counts,
     const uint64_t *__restrict__ offs, honu_acl *__restrict__ acl, uint64_t acl_cap,
     uint32_t *__restrict__ reg, uint64_t reg_cap, uint8_t *__restrict__ data, uint64_t data_cap) {
     const uint32_t r = threadIdx.x & (G - 1);
-    const uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G;
-    if (i >= n) return;
     honu_record_info *inf = info + i;
     // independent loads first (one round trip)
     const int32_t mst = inf->meta_status;
@@ -883,6 +904,18 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_grp(
     }
 }
 
+template <int G>
+__global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_grp(
+    const uint8_t *__restrict__ rec, uint64_t n, honu_meta *__restrict__ meta,
+    honu_record_info *__restrict__ info, const DecodeScratch *__restrict__ scratch,
+    const uint32_t *__restrict__ reg_inline, const uint64_t *__restrict__ counts,
+    const uint64_t *__restrict__ offs, honu_acl *__restrict__ acl, uint64_t acl_cap,
+    uint32_t *__restrict__ reg, uint64_t reg_cap, uint8_t *__restrict__ data, uint64_t data_cap) {
+    for (uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G; i < n;
+         i += (uint64_t)gridDim.x * (HONU_BLOCK / G))
+        k_decode_fill_grp_one<G>(i, rec, n, meta, info, scratch, reg_inline, counts, offs, acl, acl_cap, reg, reg_cap, data, data_cap);
+}
+
 
 // ------------------------------------------------------------------------
 // encode ACL entries (metadata.go:157-162, acls.go:26-39) into the gap the
@@ -927,13 +960,10 @@ HONU_DEV u32x4 acl_chunk(const honu_acl *A, uint64_t na, uint64_t P, uint64_t X)
 }
 
 template <int G>
-__global__ __launch_bounds__(HONU_BLOCK) void k_encode_acl_grp(
-    const honu_meta *__restrict__ meta, const honu_acl *__restrict__ acl, uint64_t n,
+HONU_DEV void k_encode_acl_grp_one(uint64_t i, const honu_meta *__restrict__ meta, const honu_acl *__restrict__ acl, uint64_t n,
     uint8_t *__restrict__ out, const int32_t *__restrict__ status,
     const uint64_t *__restrict__ acl_pos) {
     const uint32_t r = threadIdx.x & (G - 1);
-    const uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G;
-    if (i >= n) return;
     // independent loads first: one round trip before the entries
     const int32_t sti = status[i];
     const uint64_t na = meta[i].acl_count, ao = meta[i].acl_off, pos = acl_pos[i];
@@ -975,18 +1005,29 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_acl_grp(
     }
 }
 
+template <int G>
+__global__ __launch_bounds__(HONU_BLOCK) void k_encode_acl_grp(
+    const honu_meta *__restrict__ meta, const honu_acl *__restrict__ acl, uint64_t n,
+    uint8_t *__restrict__ out, const int32_t *__restrict__ status,
+    const uint64_t *__restrict__ acl_pos) {
+    for (uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G; i < n;
+         i += (uint64_t)gridDim.x * (HONU_BLOCK / G))
+        k_encode_acl_grp_one<G>(i, meta, acl, n, out, status, acl_pos);
+}
+
 #undef OFF
 
-static dim3 grp_grid(uint64_t n) {
-    return dim3((unsigned)((n * GRP + HONU_BLOCK - 1) / HONU_BLOCK));
+static dim3 grp_grid(uint64_t n, int cap) {
+    const uint64_t b = (n * GRP + HONU_BLOCK - 1) / HONU_BLOCK;
+    return dim3((unsigned)(cap > 0 && b > (uint64_t)cap ? (uint64_t)cap : b));
 }
 
 hipError_t launch_encode_sizes_grp(const honu_meta *meta, uint64_t var_len, const honu_acl *acl,
                                    uint64_t acl_len, const uint32_t *reg, uint64_t reg_len,
                                    const uint64_t *payload_off, uint64_t n, uint64_t *sizes,
-                                   int32_t *status, hipStream_t s) {
+                                   int32_t *status, int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_encode_sizes_grp<GRP>, grp_grid(n), dim3(HONU_BLOCK), 0, s, meta,
+    hipLaunchKernelGGL(k_encode_sizes_grp<GRP>, grp_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta,
                        var_len, acl, acl_len, reg, reg_len, payload_off, n, sizes, status);
     return hipGetLastError();
 }
@@ -994,18 +1035,18 @@ hipError_t launch_encode_sizes_grp(const honu_meta *meta, uint64_t var_len, cons
 hipError_t launch_encode_meta_grp(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
                                   const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
                                   uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
-                                  int32_t *status, hipStream_t s) {
+                                  int32_t *status, int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_encode_meta_grp<GRP>, grp_grid(n), dim3(HONU_BLOCK), 0, s, meta, var, acl,
+    hipLaunchKernelGGL(k_encode_meta_grp<GRP>, grp_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta, var, acl,
                        reg, payload_off, n, out, out_cap, out_off, status);
     return hipGetLastError();
 }
 
 hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uint64_t n,
                                  uint8_t *out, const int32_t *status, const uint64_t *acl_pos,
-                                 hipStream_t s) {
+                                 int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_encode_acl_grp<GRP>, grp_grid(n), dim3(HONU_BLOCK), 0, s, meta, acl, n,
+    hipLaunchKernelGGL(k_encode_acl_grp<GRP>, grp_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta, acl, n,
                        out, status, acl_pos);
     return hipGetLastError();
 }
@@ -1013,9 +1054,9 @@ hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uin
 hipError_t launch_decode_parse_grp(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                    honu_meta *meta, honu_record_info *info,
                                    DecodeScratch *scratch, uint32_t *reg_inline, uint64_t *counts,
-                                   hipStream_t s) {
+                                   int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_decode_parse_grp<GRP>, grp_grid(n), dim3(HONU_BLOCK), 0, s, rec, rec_off,
+    hipLaunchKernelGGL(k_decode_parse_grp<GRP>, grp_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, rec, rec_off,
                        n, meta, info, scratch, reg_inline, counts);
     return hipGetLastError();
 }
@@ -1025,9 +1066,9 @@ hipError_t launch_decode_fill_grp(const uint8_t *rec, uint64_t n, honu_meta *met
                                   const uint32_t *reg_inline, const uint64_t *counts,
                                   const uint64_t *offs, honu_acl *acl, uint64_t acl_cap,
                                   uint32_t *reg, uint64_t reg_cap, uint8_t *data,
-                                  uint64_t data_cap, hipStream_t s) {
+                                  uint64_t data_cap, int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_decode_fill_grp<GRP>, grp_grid(n), dim3(HONU_BLOCK), 0, s, rec, n, meta,
+    hipLaunchKernelGGL(k_decode_fill_grp<GRP>, grp_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, rec, n, meta,
                        info, scratch, reg_inline, counts, offs, acl, acl_cap, reg, reg_cap, data,
                        data_cap);
     return hipGetLastError();

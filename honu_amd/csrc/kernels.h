@@ -46,6 +46,8 @@ HONU_DEV void acl_enc_words(const honu_acl *e, uint32_t d[5]) {
 struct LaunchGeom {
     int num_cu;
     int per_record_blocks;  // cap on blocks for one-wave-per-record kernels
+    int lane_blocks;        // cap on blocks for the lane / group / window kernels
+                            // (0: one block per 256 lanes of work, no cap)
     int copy_blocks;        // blocks of the byte-balanced copy kernel
     int copy_variant;       // copy engine variant (copy.hip: unroll depth / cache policy)
     int record_variant;     // per-record kernels: 0 auto (the fastest measured form
@@ -91,49 +93,49 @@ hipError_t launch_decode_keys(const LaunchGeom &g, const honu_meta *meta,
 hipError_t launch_decode_parse_lane(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                     honu_meta *meta, honu_record_info *info,
                                     DecodeScratch *scratch, uint32_t *reg_inline,
-                                    uint64_t *counts, hipStream_t s);
+                                    uint64_t *counts, int max_blocks, hipStream_t s);
 hipError_t launch_decode_fill_lane(const uint8_t *rec, uint64_t n, honu_meta *meta,
                                    honu_record_info *info, const DecodeScratch *scratch,
                                    const uint64_t *counts, const uint64_t *offs, honu_acl *acl,
                                    uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap,
-                                   uint8_t *data, uint64_t data_cap, hipStream_t s);
+                                   uint8_t *data, uint64_t data_cap, int max_blocks, hipStream_t s);
 // acl_out != null: the ACL entries are left out (positions in acl_out) for
 // launch_encode_acl_grp
 hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
                                    const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
                                    uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
-                                   int32_t *status, uint64_t *acl_out, hipStream_t s);
+                                   int32_t *status, uint64_t *acl_out, int max_blocks, hipStream_t s);
 hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uint64_t n,
                                  uint8_t *out, const int32_t *status, const uint64_t *acl_pos,
-                                 hipStream_t s);
+                                 int max_blocks, hipStream_t s);
 hipError_t launch_encode_sizes_lane(const honu_meta *meta, uint64_t var_len, const honu_acl *acl,
                                     uint64_t acl_len, const uint32_t *reg, uint64_t reg_len,
                                     const uint64_t *payload_off, uint64_t n, uint64_t *sizes,
-                                    int32_t *status, hipStream_t s);
+                                    int32_t *status, int max_blocks, hipStream_t s);
 
 hipError_t launch_encode_sizes_grp(const honu_meta *meta, uint64_t var_len, const honu_acl *acl,
                                    uint64_t acl_len, const uint32_t *reg, uint64_t reg_len,
                                    const uint64_t *payload_off, uint64_t n, uint64_t *sizes,
-                                   int32_t *status, hipStream_t s);
+                                   int32_t *status, int max_blocks, hipStream_t s);
 hipError_t launch_encode_meta_grp(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
                                   const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
                                   uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
-                                  int32_t *status, hipStream_t s);
+                                  int32_t *status, int max_blocks, hipStream_t s);
 hipError_t launch_decode_parse_grp(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                    honu_meta *meta, honu_record_info *info,
                                    DecodeScratch *scratch, uint32_t *reg_inline, uint64_t *counts,
-                                   hipStream_t s);
+                                   int max_blocks, hipStream_t s);
 hipError_t launch_decode_fill_grp(const uint8_t *rec, uint64_t n, honu_meta *meta,
                                   honu_record_info *info, const DecodeScratch *scratch,
                                   const uint32_t *reg_inline, const uint64_t *counts,
                                   const uint64_t *offs, honu_acl *acl, uint64_t acl_cap,
                                   uint32_t *reg, uint64_t reg_cap, uint8_t *data,
-                                  uint64_t data_cap, hipStream_t s);
+                                  uint64_t data_cap, int max_blocks, hipStream_t s);
 
 hipError_t launch_decode_parse_win(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                    honu_meta *meta, honu_record_info *info,
                                    DecodeScratch *scratch, uint32_t *reg_inline, uint64_t *counts,
-                                   hipStream_t s);
+                                   int max_blocks, hipStream_t s);
 
 // Exclusive scan of K interleaved u64 columns: out[i*K+c] = sum_{j<i} in[j*K+c];
 // totals[c] = full sum. `partials` needs scan_partials_len(n, K) u64.

@@ -18,13 +18,10 @@ namespace honu {
 // decode parse: Object.Metadata() + Data() + Tombstone() + StorageVersion()
 // (object.go:47-134) with the lani walk of metadata.go:202-302.
 // ------------------------------------------------------------------------
-__global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_lane(
-    const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
+HONU_DEV void k_decode_parse_lane_one(uint64_t i, const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
     honu_meta *__restrict__ meta, honu_record_info *__restrict__ info,
     DecodeScratch *__restrict__ scratch, uint32_t *__restrict__ reg_inline,
     uint64_t *__restrict__ counts) {
-    const uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x;
-    if (i >= n) return;
     const uint64_t beg = rec_off[i], end = rec_off[i + 1];
     const uint64_t len = end - beg;
     uint32_t ver = 0;
@@ -210,17 +207,24 @@ done:
     counts[3 * i + 2] = (data_len + 15) & ~15ull;
 }
 
+__global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_lane(
+    const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
+    honu_meta *__restrict__ meta, honu_record_info *__restrict__ info,
+    DecodeScratch *__restrict__ scratch, uint32_t *__restrict__ reg_inline,
+    uint64_t *__restrict__ counts) {
+    for (uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * HONU_BLOCK)
+        k_decode_parse_lane_one(i, rec, rec_off, n, meta, info, scratch, reg_inline, counts);
+}
+
 // ------------------------------------------------------------------------
 // decode fill: ACL/region tables and offsets (after the count scans)
 // ------------------------------------------------------------------------
-__global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_lane(
-    const uint8_t *__restrict__ rec, uint64_t n, honu_meta *__restrict__ meta,
+HONU_DEV void k_decode_fill_lane_one(uint64_t i, const uint8_t *__restrict__ rec, uint64_t n, honu_meta *__restrict__ meta,
     honu_record_info *__restrict__ info, const DecodeScratch *__restrict__ scratch,
     const uint64_t *__restrict__ counts, const uint64_t *__restrict__ offs,
     honu_acl *__restrict__ acl, uint64_t acl_cap, uint32_t *__restrict__ reg, uint64_t reg_cap,
     uint8_t *__restrict__ data, uint64_t data_cap) {
-    const uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x;
-    if (i >= n) return;
     honu_record_info *inf = info + i;
     if (inf->meta_status == HONU_OK) {
         const uint64_t na = counts[3 * i], nr = counts[3 * i + 1];
@@ -298,6 +302,17 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_lane(
     }
 }
 
+__global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_lane(
+    const uint8_t *__restrict__ rec, uint64_t n, honu_meta *__restrict__ meta,
+    honu_record_info *__restrict__ info, const DecodeScratch *__restrict__ scratch,
+    const uint64_t *__restrict__ counts, const uint64_t *__restrict__ offs,
+    honu_acl *__restrict__ acl, uint64_t acl_cap, uint32_t *__restrict__ reg, uint64_t reg_cap,
+    uint8_t *__restrict__ data, uint64_t data_cap) {
+    for (uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * HONU_BLOCK)
+        k_decode_fill_lane_one(i, rec, n, meta, info, scratch, counts, offs, acl, acl_cap, reg, reg_cap, data, data_cap);
+}
+
 // ------------------------------------------------------------------------
 // encode size pass: exact record length (object.go:24-45 / App. A)
 // ------------------------------------------------------------------------
@@ -306,13 +321,10 @@ HONU_DEV bool span_in(uint64_t off, uint64_t len, uint64_t var_len) {
 }
 HONU_DEV uint64_t frame_len(uint64_t len) { return uvarint_len(len) + len; }
 
-__global__ __launch_bounds__(HONU_BLOCK) void k_encode_sizes_lane(
-    const honu_meta *__restrict__ meta, uint64_t var_len, const honu_acl *__restrict__ acl,
+HONU_DEV void k_encode_sizes_lane_one(uint64_t i, const honu_meta *__restrict__ meta, uint64_t var_len, const honu_acl *__restrict__ acl,
     uint64_t acl_len, const uint32_t *__restrict__ reg, uint64_t reg_len,
     const uint64_t *__restrict__ payload_off, uint64_t n, uint64_t *__restrict__ sizes,
     int32_t *__restrict__ status) {
-    const uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x;
-    if (i >= n) return;
     const honu_meta &m = meta[i];
     const uint32_t pr = m.present;
     uint64_t size = 0;
@@ -379,6 +391,16 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_sizes_lane(
     if (status) status[i] = st;
 }
 
+__global__ __launch_bounds__(HONU_BLOCK) void k_encode_sizes_lane(
+    const honu_meta *__restrict__ meta, uint64_t var_len, const honu_acl *__restrict__ acl,
+    uint64_t acl_len, const uint32_t *__restrict__ reg, uint64_t reg_len,
+    const uint64_t *__restrict__ payload_off, uint64_t n, uint64_t *__restrict__ sizes,
+    int32_t *__restrict__ status) {
+    for (uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * HONU_BLOCK)
+        k_encode_sizes_lane_one(i, meta, var_len, acl, acl_len, reg, reg_len, payload_off, n, sizes, status);
+}
+
 // ------------------------------------------------------------------------
 // encode: header + Metadata tail (object.go:24-45, metadata.go:108-200)
 // ------------------------------------------------------------------------
@@ -388,14 +410,11 @@ HONU_DEV uint64_t ld64(const uint8_t *p) { return *reinterpret_cast<const uint64
 // fields up to uvarint(len ACL), record that position in acl_out[i], and
 // resume at end - (bytes after the list), computed from the row and regions.
 template <bool SKIP_ACL>
-__global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
-    const honu_meta *__restrict__ meta, const uint8_t *__restrict__ var,
+HONU_DEV void k_encode_meta_lane_one(uint64_t i, const honu_meta *__restrict__ meta, const uint8_t *__restrict__ var,
     const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
     const uint64_t *__restrict__ payload_off, uint64_t n, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status,
     uint64_t *__restrict__ acl_out) {
-    const uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x;
-    if (i >= n) return;
     if (status[i] != HONU_OK) return;
     const uint64_t beg = out_off[i], end = out_off[i + 1];
     if (end > out_cap) {
@@ -574,17 +593,32 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
     W.finish();
 }
 
+template <bool SKIP_ACL>
+__global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
+    const honu_meta *__restrict__ meta, const uint8_t *__restrict__ var,
+    const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
+    const uint64_t *__restrict__ payload_off, uint64_t n, uint8_t *__restrict__ out,
+    uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status,
+    uint64_t *__restrict__ acl_out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * HONU_BLOCK)
+        k_encode_meta_lane_one<SKIP_ACL>(i, meta, var, acl, reg, payload_off, n, out, out_cap, out_off, status, acl_out);
+}
+
 #undef TRY
 #undef OFF
 
-static dim3 lane_grid(uint64_t n) { return dim3((unsigned)((n + HONU_BLOCK - 1) / HONU_BLOCK)); }
+static dim3 lane_grid(uint64_t n, int cap) {
+    const uint64_t b = (n + HONU_BLOCK - 1) / HONU_BLOCK;
+    return dim3((unsigned)(cap > 0 && b > (uint64_t)cap ? (uint64_t)cap : b));
+}
 
 hipError_t launch_decode_parse_lane(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                     honu_meta *meta, honu_record_info *info,
                                     DecodeScratch *scratch, uint32_t *reg_inline,
-                                    uint64_t *counts, hipStream_t s) {
+                                    uint64_t *counts, int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_decode_parse_lane, lane_grid(n), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
+    hipLaunchKernelGGL(k_decode_parse_lane, lane_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
                        meta, info, scratch, reg_inline, counts);
     return hipGetLastError();
 }
@@ -593,9 +627,9 @@ hipError_t launch_decode_fill_lane(const uint8_t *rec, uint64_t n, honu_meta *me
                                    honu_record_info *info, const DecodeScratch *scratch,
                                    const uint64_t *counts, const uint64_t *offs, honu_acl *acl,
                                    uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap,
-                                   uint8_t *data, uint64_t data_cap, hipStream_t s) {
+                                   uint8_t *data, uint64_t data_cap, int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_decode_fill_lane, lane_grid(n), dim3(HONU_BLOCK), 0, s, rec, n, meta, info,
+    hipLaunchKernelGGL(k_decode_fill_lane, lane_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, rec, n, meta, info,
                        scratch, counts, offs, acl, acl_cap, reg, reg_cap, data, data_cap);
     return hipGetLastError();
 }
@@ -603,9 +637,9 @@ hipError_t launch_decode_fill_lane(const uint8_t *rec, uint64_t n, honu_meta *me
 hipError_t launch_encode_sizes_lane(const honu_meta *meta, uint64_t var_len, const honu_acl *acl,
                                     uint64_t acl_len, const uint32_t *reg, uint64_t reg_len,
                                     const uint64_t *payload_off, uint64_t n, uint64_t *sizes,
-                                    int32_t *status, hipStream_t s) {
+                                    int32_t *status, int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_encode_sizes_lane, lane_grid(n), dim3(HONU_BLOCK), 0, s, meta, var_len,
+    hipLaunchKernelGGL(k_encode_sizes_lane, lane_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta, var_len,
                        acl, acl_len, reg, reg_len, payload_off, n, sizes, status);
     return hipGetLastError();
 }
@@ -616,13 +650,13 @@ namespace honu {
 hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
                                    const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
                                    uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
-                                   int32_t *status, uint64_t *acl_out, hipStream_t s) {
+                                   int32_t *status, uint64_t *acl_out, int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (acl_out)
-        hipLaunchKernelGGL(k_encode_meta_lane<true>, lane_grid(n), dim3(HONU_BLOCK), 0, s, meta,
+        hipLaunchKernelGGL(k_encode_meta_lane<true>, lane_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta,
                            var, acl, reg, payload_off, n, out, out_cap, out_off, status, acl_out);
     else
-        hipLaunchKernelGGL(k_encode_meta_lane<false>, lane_grid(n), dim3(HONU_BLOCK), 0, s, meta,
+        hipLaunchKernelGGL(k_encode_meta_lane<false>, lane_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta,
                            var, acl, reg, payload_off, n, out, out_cap, out_off, status, acl_out);
     return hipGetLastError();
 }

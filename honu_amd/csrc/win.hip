@@ -150,16 +150,13 @@ struct WDec {  // lani.Decoder (lani/decode.go) over [tstart, end), as LaneDec
     } while (0)
 #define HONU_SKIP 0x7fffffff  // lane without a walk (past n, or header error)
 
-__global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_win(
-    const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
-    honu_meta *__restrict__ meta, honu_record_info *__restrict__ info,
-    DecodeScratch *__restrict__ scratch, uint32_t *__restrict__ reg_inline,
-    uint64_t *__restrict__ counts) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * WIN_WAVE_BYTES];
+HONU_DEV void parse_win_one(
+    uint64_t i0, uint8_t *smem, const uint8_t *__restrict__ rec,
+    const uint64_t *__restrict__ rec_off, uint64_t n, honu_meta *__restrict__ meta,
+    honu_record_info *__restrict__ info, DecodeScratch *__restrict__ scratch,
+    uint32_t *__restrict__ reg_inline, uint64_t *__restrict__ counts) {
     const uint32_t lane = lane_id();
     const uint32_t wv = threadIdx.x / HONU_WAVE;
-    const uint64_t i0 = (uint64_t)blockIdx.x * HONU_BLOCK + wv * HONU_WAVE;  // wave's first record
-    if (i0 >= n) return;  // whole wave
     const uint64_t i = i0 + lane;
     const bool valid = i < n;
     LaneWin W;
@@ -391,15 +388,33 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_win(
     counts[3 * i + 2] = (data_len + 15) & ~15ull;
 }
 
+// one wave per 64 records, grid-stride over the batch (the loop is wave-uniform)
+__global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_win(
+    const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
+    honu_meta *__restrict__ meta, honu_record_info *__restrict__ info,
+    DecodeScratch *__restrict__ scratch, uint32_t *__restrict__ reg_inline,
+    uint64_t *__restrict__ counts) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * WIN_WAVE_BYTES];
+    const uint32_t wv = threadIdx.x / HONU_WAVE;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * HONU_BLOCK + wv * HONU_WAVE; i0 < n;
+         i0 += (uint64_t)gridDim.x * HONU_BLOCK)
+        parse_win_one(i0, smem, rec, rec_off, n, meta, info, scratch, reg_inline, counts);
+}
+
 #undef STEP
 #undef OFF
+
+static dim3 win_grid(uint64_t n, int cap) {
+    const uint64_t b = (n + HONU_BLOCK - 1) / HONU_BLOCK;
+    return dim3((unsigned)(cap > 0 && b > (uint64_t)cap ? (uint64_t)cap : b));
+}
 
 hipError_t launch_decode_parse_win(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                    honu_meta *meta, honu_record_info *info,
                                    DecodeScratch *scratch, uint32_t *reg_inline, uint64_t *counts,
-                                   hipStream_t s) {
+                                   int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_decode_parse_win, dim3((unsigned)((n + HONU_BLOCK - 1) / HONU_BLOCK)),
+    hipLaunchKernelGGL(k_decode_parse_win, win_grid(n, max_blocks),
                        dim3(HONU_BLOCK), 0, s, rec, rec_off, n, meta, info, scratch, reg_inline,
                        counts);
     return hipGetLastError();

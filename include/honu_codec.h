@@ -188,12 +188,14 @@ uint64_t honu_ctx_max_records(const honu_ctx *ctx);
 /* Launch-geometry knobs (defaults suit MI355X): "copy_blocks" (workgroups of
  * the payload copy kernel, default 2 per CU), "record_blocks" (cap on
  * workgroups of the one-wave-per-record kernels, default 8 per CU),
+ * "lane_blocks" (cap on workgroups of the lane, group and window kernels;
+ * default 0 = no cap — a cap leaves room for a concurrent payload copy),
  * "copy_variant" (copy-engine variant, default 0), "record_variant" (how the
  * per-record metadata kernels map records to lanes: 0 auto — the fastest
  * measured form per kernel, 1 one record per wave, 2 one record per group of
  * 16 lanes, 3 one record per lane). Also
  * settable at context creation through the environment (HONU_COPY_BLOCKS,
- * HONU_RECORD_BLOCKS, HONU_COPY_VARIANT, HONU_RECORD_VARIANT). */
+ * HONU_RECORD_BLOCKS, HONU_LANE_BLOCKS, HONU_COPY_VARIANT, HONU_RECORD_VARIANT). */
 int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value);
 
 /* ABI self-description, used by bindings to check struct layouts. */
