@@ -25,6 +25,8 @@ _PROTOS = {
     "honu_sizeof_meta": (U64, []),
     "honu_sizeof_acl": (U64, []),
     "honu_sizeof_record_info": (U64, []),
+    "honu_sizeof_collection": (U64, []),
+    "honu_sizeof_index": (U64, []),
     "honu_status_string": (C.c_char_p, [I32]),
     "honu_last_error": (C.c_char_p, []),
     "honu_ctx_create": (P, [C.c_int, U64, C.POINTER(I32)]),
@@ -43,6 +45,11 @@ _PROTOS = {
     "honu_decode_fill": (I32, [P, P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),
     "honu_decode_batch": (I32, [P, P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),
     "honu_decode_keys": (I32, [P, P, P, U64, P, P, P]),
+    "honu_system_sizes": (I32, [P, P, U64, P, U64, P, U64, P, U64, U64, P, P, P]),
+    "honu_system_encode": (I32, [P, P, P, P, P, P, U64, P, U64, P, P, P]),
+    "honu_system_marshal_batch": (I32, [P, P, P, U64, P, U64, P, U64, P, U64, U64, P, U64, P, P,
+                                        P]),
+    "honu_system_decode_batch": (I32, [P, P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),
     "honu_gen_totals": (None, [U64, I32, U64, U64, P]),
     "honu_gen_meta": (None, [U64, I32, U64, U64, P, P, P, P, P]),
     "honu_gen_payload_host": (None, [U64, U64, U64, P, P]),

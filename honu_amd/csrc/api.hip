@@ -55,6 +55,8 @@ extern "C" {
 uint32_t honu_abi_version(void) { return HONU_ABI_VERSION; }
 uint64_t honu_sizeof_meta(void) { return sizeof(honu_meta); }
 uint64_t honu_sizeof_acl(void) { return sizeof(honu_acl); }
+uint64_t honu_sizeof_collection(void) { return sizeof(honu_collection); }
+uint64_t honu_sizeof_index(void) { return sizeof(honu_index); }
 uint64_t honu_sizeof_record_info(void) { return sizeof(honu_record_info); }
 const char *honu_last_error(void) { return g_last_error; }
 
@@ -370,6 +372,78 @@ int32_t honu_decode_keys(honu_ctx *ctx, const honu_meta *d_meta, const honu_reco
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(launch_decode_keys(ctx->geom, d_meta, d_info, n, d_keys, d_key_status,
                               (hipStream_t)stream));
+    return HONU_OK;
+}
+
+// ---------------------------------------------------------------------------
+// system objects (object/system.go)
+// ---------------------------------------------------------------------------
+int32_t honu_system_sizes(honu_ctx *ctx, const honu_collection *d_rows, uint64_t var_len,
+                          const honu_acl *d_acl, uint64_t acl_len, const uint32_t *d_regions,
+                          uint64_t regions_len, const honu_index *d_index, uint64_t index_len,
+                          uint64_t n, uint64_t *d_sizes, int32_t *d_status, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n && (!d_rows || !d_sizes)) return arg_fail("null pointer");
+    if (!aligned(d_acl, 4) || !aligned(d_regions, 4) || !aligned(d_index, 8))
+        return arg_fail("tables must be aligned");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_system_sizes(d_rows, var_len, d_acl, acl_len, d_regions, regions_len, d_index,
+                               index_len, n, d_sizes, d_status, (hipStream_t)stream));
+    return HONU_OK;
+}
+
+int32_t honu_system_encode(honu_ctx *ctx, const honu_collection *d_rows, const uint8_t *d_var,
+                           const honu_acl *d_acl, const uint32_t *d_regions,
+                           const honu_index *d_index, uint64_t n, uint8_t *d_out,
+                           uint64_t out_cap, const uint64_t *d_out_off, int32_t *d_status,
+                           void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n && (!d_rows || !d_out || !d_out_off || !d_status)) return arg_fail("null pointer");
+    if (!aligned(d_acl, 4) || !aligned(d_regions, 4) || !aligned(d_index, 8))
+        return arg_fail("tables must be aligned");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_system_encode(d_rows, d_var, d_acl, d_regions, d_index, n, d_out, out_cap,
+                                d_out_off, d_status, (hipStream_t)stream));
+    return HONU_OK;
+}
+
+int32_t honu_system_marshal_batch(honu_ctx *ctx, const honu_collection *d_rows,
+                                  const uint8_t *d_var, uint64_t var_len, const honu_acl *d_acl,
+                                  uint64_t acl_len, const uint32_t *d_regions,
+                                  uint64_t regions_len, const honu_index *d_index,
+                                  uint64_t index_len, uint64_t n, uint8_t *d_out,
+                                  uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status,
+                                  void *stream) {
+    int32_t st = honu_system_sizes(ctx, d_rows, var_len, d_acl, acl_len, d_regions, regions_len,
+                                   d_index, index_len, n, d_out_off, d_status, stream);
+    if (st) return st;
+    st = honu_exclusive_scan(ctx, d_out_off, n, d_out_off, stream);
+    if (st) return st;
+    return honu_system_encode(ctx, d_rows, d_var, d_acl, d_regions, d_index, n, d_out, out_cap,
+                              d_out_off, d_status, stream);
+}
+
+int32_t honu_system_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                                 uint64_t n, honu_collection *d_rows, int32_t *d_status,
+                                 honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
+                                 uint64_t regions_cap, honu_index *d_index, uint64_t index_cap,
+                                 uint64_t *d_totals, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n > ctx->max_n) return HONU_E_WORKSPACE;
+    if (n && (!d_rec || !d_rec_off || !d_rows || !d_status)) return arg_fail("null pointer");
+    if (!aligned(d_rows, 16) || !aligned(d_acl, 4) || !aligned(d_regions, 4) ||
+        !aligned(d_index, 8))
+        return arg_fail("rows 16-byte / tables 4- and 8-byte aligned");
+    if ((acl_cap && !d_acl) || (regions_cap && !d_regions) || (index_cap && !d_index))
+        return arg_fail("table");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    uint64_t *tot = d_totals ? d_totals : ctx->totals;
+    HIPCHK(launch_system_parse(d_rec, d_rec_off, n, d_rows, d_status, ctx->scratch, ctx->counts,
+                               s));
+    HIPCHK(launch_scan(ctx->counts, n, 3, ctx->offs, tot, ctx->partials, s));
+    HIPCHK(launch_system_fill(d_rec, n, d_rows, d_status, ctx->scratch, ctx->counts, ctx->offs,
+                              d_acl, acl_cap, d_regions, regions_cap, d_index, index_cap, s));
     return HONU_OK;
 }
 

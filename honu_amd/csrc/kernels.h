@@ -137,6 +137,23 @@ hipError_t launch_decode_parse_win(const uint8_t *rec, const uint64_t *rec_off, 
                                    DecodeScratch *scratch, uint32_t *reg_inline, uint64_t *counts,
                                    int max_blocks, hipStream_t s);
 
+hipError_t launch_system_sizes(const honu_collection *rows, uint64_t var_len, const honu_acl *acl,
+                               uint64_t acl_len, const uint32_t *reg, uint64_t reg_len,
+                               const honu_index *idx, uint64_t idx_len, uint64_t n,
+                               uint64_t *sizes, int32_t *status, hipStream_t s);
+hipError_t launch_system_encode(const honu_collection *rows, const uint8_t *var,
+                                const honu_acl *acl, const uint32_t *reg, const honu_index *idx,
+                                uint64_t n, uint8_t *out, uint64_t out_cap,
+                                const uint64_t *out_off, int32_t *status, hipStream_t s);
+hipError_t launch_system_parse(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                               honu_collection *rows, int32_t *status, DecodeScratch *scratch,
+                               uint64_t *counts, hipStream_t s);
+hipError_t launch_system_fill(const uint8_t *rec, uint64_t n, honu_collection *rows,
+                              int32_t *status, const DecodeScratch *scratch,
+                              const uint64_t *counts, const uint64_t *offs, honu_acl *acl,
+                              uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap, honu_index *idx,
+                              uint64_t idx_cap, hipStream_t s);
+
 // Exclusive scan of K interleaved u64 columns: out[i*K+c] = sum_{j<i} in[j*K+c];
 // totals[c] = full sum. `partials` needs scan_partials_len(n, K) u64.
 uint64_t scan_partials_len(uint64_t n, int K);

@@ -82,12 +82,13 @@ HONU_DEV uint32_t uvarint_window(uint64_t lo, uint64_t hi, uint32_t n, uint64_t 
     return k;
 }
 
-// Row image in registers: 88 dwords of honu_meta, indices static.
-struct Row {
-    uint32_t d[88];
+// Row image in registers (NDW dwords: 88 for honu_meta, 92 for
+// honu_collection), indices static.
+template <int NDW> struct RowT {
+    uint32_t d[NDW];
     HONU_DEV void clear() {
 #pragma unroll
-        for (int i = 0; i < 88; i++) d[i] = 0;
+        for (int i = 0; i < NDW; i++) d[i] = 0;
     }
     HONU_DEV void u8(int off, uint32_t v) { d[off >> 2] |= (v & 0xFF) << (8 * (off & 3)); }
     HONU_DEV void u32(int off, uint32_t v) { d[off >> 2] = v; }
@@ -103,12 +104,15 @@ struct Row {
         u64(off, o);
         u64(off + 8, l);
     }
-    HONU_DEV void store(honu_meta *dst) const {
+    template <class T> HONU_DEV void store(T *dst) const {
+        static_assert(sizeof(T) == 4 * NDW, "row size");
         u32x4 *p = reinterpret_cast<u32x4 *>(dst);
 #pragma unroll
-        for (int i = 0; i < 22; i++) p[i] = u32x4{d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]};
+        for (int i = 0; i < NDW / 4; i++)
+            p[i] = u32x4{d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]};
     }
 };
+using Row = RowT<88>;
 
 // lani.Decoder (lani/decode.go) over [tstart, end) for one lane.
 struct LaneDec {

@@ -182,6 +182,69 @@ class HostBatch:
         return len(self.meta)
 
 
+def pack_common(r, m, span, acl_rows: list, regions: list) -> int:
+    """Fill the row fields Metadata and Collection share (Version, Schema,
+    Owner, Group, Permissions, ACL, WriteRegions, Publisher, Encryption,
+    Compression, Flags, Created, Modified); returns their presence bits."""
+    pr = 0
+    if m.Version is not None:
+        v = m.Version
+        pr |= HAS_VERSION
+        r["pid"], r["vid"], r["region"] = v.Scalar.PID, v.Scalar.VID, v.Region
+        r["tombstone"] = 1 if v.Tombstone else 0
+        r["version_created"] = v.Created
+        if v.Parent is not None:
+            pr |= HAS_PARENT
+            r["parent_pid"], r["parent_vid"] = v.Parent.PID, v.Parent.VID
+    if m.Schema is not None:
+        pr |= HAS_SCHEMA
+        r["schema_name"] = span(_s2b(m.Schema.Name))
+        r["schema_major"], r["schema_minor"], r["schema_patch"] = (
+            m.Schema.Major, m.Schema.Minor, m.Schema.Patch)
+    r["owner"] = np.frombuffer(_ulid(m.Owner), np.uint8)
+    r["group"] = np.frombuffer(_ulid(m.Group), np.uint8)
+    r["permissions"] = m.Permissions
+    if m.ACL:
+        r["acl_off"], r["acl_count"] = len(acl_rows), len(m.ACL)
+        for a in m.ACL:
+            acl_rows.append(None if a is None else (_ulid(a.ClientID), a.Permissions))
+    if m.WriteRegions:
+        r["regions_off"], r["regions_count"] = len(regions), len(m.WriteRegions)
+        regions.extend(m.WriteRegions)
+    if m.Publisher is not None:
+        p = m.Publisher
+        pr |= HAS_PUBLISHER
+        r["publisher_id"] = np.frombuffer(_ulid(p.PublisherID), np.uint8)
+        r["client_id"] = np.frombuffer(_ulid(p.ClientID), np.uint8)
+        r["ip_address"] = span(_s2b(p.IPAddress))
+        r["user_agent"] = span(_s2b(p.UserAgent))
+    if m.Encryption is not None:
+        e = m.Encryption
+        pr |= HAS_ENCRYPTION
+        r["public_key_id"] = span(_s2b(e.PublicKeyID))
+        r["encryption_key"] = span(_s2b(e.EncryptionKey))
+        r["hmac_secret"] = span(_s2b(e.HMACSecret))
+        r["signature"] = span(_s2b(e.Signature))
+        r["sealing_alg"], r["encryption_alg"], r["signature_alg"] = (
+            e.SealingAlgorithm, e.EncryptionAlgorithm, e.SignatureAlgorithm)
+    if m.Compression is not None:
+        pr |= HAS_COMPRESSION
+        r["compression_alg"], r["compression_level"] = m.Compression.Algorithm, m.Compression.Level
+    r["flags"] = m.Flags
+    r["created"], r["modified"] = m.Created, m.Modified
+    return pr
+
+
+def acl_table(acl_rows: list) -> np.ndarray:
+    acl = np.zeros(len(acl_rows), ACL_DTYPE)
+    for j, a in enumerate(acl_rows):
+        if a is not None:
+            acl[j]["client_id"] = np.frombuffer(a[0], np.uint8)
+            acl[j]["permissions"] = a[1]
+            acl[j]["present"] = 1
+    return acl
+
+
 def pack_batch(metas: Sequence[Optional[Metadata]], datas: Sequence[Optional[bytes]]) -> HostBatch:
     """Flatten (meta, data) pairs into rows + arenas. A None meta is Marshal(nil, …)."""
     if len(metas) != len(datas):
@@ -201,63 +264,12 @@ def pack_batch(metas: Sequence[Optional[Metadata]], datas: Sequence[Optional[byt
         r = rows[i]
         if m is None:
             continue
-        pr = HAS_META
         r["object_id"] = np.frombuffer(_ulid(m.ObjectID), np.uint8)
         r["collection_id"] = np.frombuffer(_ulid(m.CollectionID), np.uint8)
-        if m.Version is not None:
-            v = m.Version
-            pr |= HAS_VERSION
-            r["pid"], r["vid"], r["region"] = v.Scalar.PID, v.Scalar.VID, v.Region
-            r["tombstone"] = 1 if v.Tombstone else 0
-            r["version_created"] = v.Created
-            if v.Parent is not None:
-                pr |= HAS_PARENT
-                r["parent_pid"], r["parent_vid"] = v.Parent.PID, v.Parent.VID
-        if m.Schema is not None:
-            pr |= HAS_SCHEMA
-            r["schema_name"] = span(_s2b(m.Schema.Name))
-            r["schema_major"], r["schema_minor"], r["schema_patch"] = (
-                m.Schema.Major, m.Schema.Minor, m.Schema.Patch)
         r["mime"] = span(_s2b(m.MIME))
-        r["owner"] = np.frombuffer(_ulid(m.Owner), np.uint8)
-        r["group"] = np.frombuffer(_ulid(m.Group), np.uint8)
-        r["permissions"] = m.Permissions
-        if m.ACL:
-            r["acl_off"], r["acl_count"] = len(acl_rows), len(m.ACL)
-            for a in m.ACL:
-                acl_rows.append(None if a is None else (_ulid(a.ClientID), a.Permissions))
-        if m.WriteRegions:
-            r["regions_off"], r["regions_count"] = len(regions), len(m.WriteRegions)
-            regions.extend(m.WriteRegions)
-        if m.Publisher is not None:
-            p = m.Publisher
-            pr |= HAS_PUBLISHER
-            r["publisher_id"] = np.frombuffer(_ulid(p.PublisherID), np.uint8)
-            r["client_id"] = np.frombuffer(_ulid(p.ClientID), np.uint8)
-            r["ip_address"] = span(_s2b(p.IPAddress))
-            r["user_agent"] = span(_s2b(p.UserAgent))
-        if m.Encryption is not None:
-            e = m.Encryption
-            pr |= HAS_ENCRYPTION
-            r["public_key_id"] = span(_s2b(e.PublicKeyID))
-            r["encryption_key"] = span(_s2b(e.EncryptionKey))
-            r["hmac_secret"] = span(_s2b(e.HMACSecret))
-            r["signature"] = span(_s2b(e.Signature))
-            r["sealing_alg"], r["encryption_alg"], r["signature_alg"] = (
-                e.SealingAlgorithm, e.EncryptionAlgorithm, e.SignatureAlgorithm)
-        if m.Compression is not None:
-            pr |= HAS_COMPRESSION
-            r["compression_alg"], r["compression_level"] = m.Compression.Algorithm, m.Compression.Level
-        r["flags"] = m.Flags
-        r["created"], r["modified"] = m.Created, m.Modified
-        r["present"] = pr
+        r["present"] = HAS_META | pack_common(r, m, span, acl_rows, regions)
 
-    acl = np.zeros(len(acl_rows), ACL_DTYPE)
-    for j, a in enumerate(acl_rows):
-        if a is not None:
-            acl[j]["client_id"] = np.frombuffer(a[0], np.uint8)
-            acl[j]["permissions"] = a[1]
-            acl[j]["present"] = 1
+    acl = acl_table(acl_rows)
     payload_off = np.zeros(n + 1, np.uint64)
     pay = bytearray()
     for i, d in enumerate(datas):
@@ -297,6 +309,14 @@ def unpack_row(row, arena, acl_table=None, regions_table=None) -> Metadata:
 
     m.ObjectID = bytes(row["object_id"])
     m.CollectionID = bytes(row["collection_id"])
+    m.MIME = ss("mime")
+    unpack_common(row, m, sb, ss, acl_table, regions_table)
+    return m
+
+
+def unpack_common(row, m, sb, ss, acl_table, regions_table):
+    """Inverse of pack_common on a decoded row (Go decoder nil/empty rules)."""
+    pr = int(row["present"])
     if pr & HAS_VERSION:
         m.Version = Version(Scalar(int(row["pid"]), int(row["vid"])), int(row["region"]),
                             Scalar(int(row["parent_pid"]), int(row["parent_vid"]))
@@ -305,7 +325,6 @@ def unpack_row(row, arena, acl_table=None, regions_table=None) -> Metadata:
     if pr & HAS_SCHEMA:
         m.Schema = SchemaVersion(ss("schema_name"), int(row["schema_major"]),
                                  int(row["schema_minor"]), int(row["schema_patch"]))
-    m.MIME = ss("mime")
     m.Owner = bytes(row["owner"])
     m.Group = bytes(row["group"])
     m.Permissions = int(row["permissions"])
@@ -333,7 +352,6 @@ def unpack_row(row, arena, acl_table=None, regions_table=None) -> Metadata:
     m.Flags = int(row["flags"])
     m.Created = int(row["created"])
     m.Modified = int(row["modified"])
-    return m
 
 
 def normalize(m: Optional[Metadata]) -> Optional[Metadata]:

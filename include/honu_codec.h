@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define HONU_ABI_VERSION 1u
+#define HONU_ABI_VERSION 2u
 #define HONU_STORAGE_VERSION 1u /* object.StorageVersion, object.go:14 */
 #define HONU_ULID_LEN 16
 #define HONU_KEY_LEN 29         /* keys.keySize, keys/keys.go:14 */
@@ -202,6 +202,8 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value);
 uint32_t honu_abi_version(void);
 uint64_t honu_sizeof_meta(void);
 uint64_t honu_sizeof_acl(void);
+uint64_t honu_sizeof_collection(void);
+uint64_t honu_sizeof_index(void);
 uint64_t honu_sizeof_record_info(void);
 const char *honu_status_string(int32_t status);
 /* Text of the last call-level failure on this thread (HIP error text etc.). */
@@ -307,6 +309,126 @@ int32_t honu_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
  * when the decoded Version is nil (metadata.go:54 dereferences it). */
 int32_t honu_decode_keys(honu_ctx *ctx, const honu_meta *d_meta, const honu_record_info *d_info,
                          uint64_t n, uint8_t *d_keys, int32_t *d_key_status, void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* System objects (object/system.go): metadata.Collection with its Indexes.  */
+/* ------------------------------------------------------------------------ */
+
+/* Presence bit 0 of honu_collection.present: the EncodeStruct flag that
+ * MarshalSystem writes for the collection (system.go:22); bits 1-7 as for
+ * honu_meta (Version, Parent, Schema, Publisher, Encryption, Compression,
+ * non-nil WriteRegions). */
+#define HONU_HAS_COLLECTION HONU_HAS_META
+
+/* One metadata.Collection (collection.go:16-33) as a fixed 352-byte row.
+ * Field meanings, spans, list descriptors and time encoding as honu_meta;
+ * index_off/index_count describe Collection.Indexes in a honu_index table. */
+typedef struct honu_collection {
+    uint32_t present;            /*   0 HONU_HAS_* bits */
+    uint8_t permissions;         /*   4 Collection.Permissions */
+    uint8_t flags;               /*   5 Collection.Flags */
+    uint8_t tombstone;           /*   6 Version.Tombstone */
+    uint8_t compression_alg;     /*   7 */
+    uint8_t sealing_alg;         /*   8 */
+    uint8_t encryption_alg;      /*   9 */
+    uint8_t signature_alg;       /*  10 */
+    uint8_t _pad0;               /*  11 */
+    uint32_t region;             /*  12 Version.Region */
+    uint64_t vid;                /*  16 */
+    uint32_t pid;                /*  24 */
+    uint32_t parent_pid;         /*  28 */
+    uint64_t parent_vid;         /*  32 */
+    int64_t version_created;     /*  40 */
+    uint32_t schema_major;       /*  48 */
+    uint32_t schema_minor;       /*  52 */
+    uint32_t schema_patch;       /*  56 */
+    uint32_t _pad1;              /*  60 */
+    int64_t compression_level;   /*  64 */
+    int64_t created;             /*  72 Collection.Created */
+    int64_t modified;            /*  80 Collection.Modified */
+    uint64_t _pad2;              /*  88 */
+    uint8_t id[16];              /*  96 Collection.ID */
+    uint8_t owner[16];           /* 112 */
+    uint8_t group[16];           /* 128 */
+    uint8_t publisher_id[16];    /* 144 */
+    uint8_t client_id[16];       /* 160 */
+    uint8_t _pad3[16];           /* 176 */
+    honu_span name;              /* 192 Collection.Name */
+    honu_span schema_name;       /* 208 */
+    honu_span ip_address;        /* 224 */
+    honu_span user_agent;        /* 240 */
+    honu_span public_key_id;     /* 256 */
+    honu_span encryption_key;    /* 272 */
+    honu_span hmac_secret;       /* 288 */
+    honu_span signature;         /* 304 */
+    uint64_t acl_off;            /* 320 */
+    uint64_t acl_count;          /* 328 len(ACL); 0 <=> nil */
+    uint64_t regions_off;        /* 336 */
+    uint64_t regions_count;      /* 344 */
+    uint64_t index_off;          /* 352 first entry in the index table */
+    uint64_t index_count;        /* 360 len(Indexes); 0 <=> nil */
+} honu_collection;               /* 368 */
+
+/* One *metadata.Index (index.go:16-22) with its Field / Ref (field.go:12-16).
+ * present == 0 is a nil pointer in the Indexes slice. */
+typedef struct honu_index {
+    uint8_t present;             /*   0 */
+    uint8_t type;                /*   1 IndexType */
+    uint8_t has_field;           /*   2 Field != nil */
+    uint8_t field_type;          /*   3 Field.Type (FieldType) */
+    uint8_t has_ref;             /*   4 Ref != nil */
+    uint8_t ref_type;            /*   5 Ref.Type */
+    uint8_t _pad[10];            /*   6 */
+    uint8_t id[16];              /*  16 Index.ID */
+    uint8_t field_collection[16];/*  32 Field.Collection */
+    uint8_t ref_collection[16];  /*  48 Ref.Collection */
+    honu_span name;              /*  64 Index.Name */
+    honu_span field_name;        /*  80 Field.Name */
+    honu_span ref_name;          /*  96 Ref.Name */
+} honu_index;                    /* 112 */
+
+/* ------------------------------------------------------------------------ */
+/* System objects on the GPU                                                 */
+/* ------------------------------------------------------------------------ */
+
+/* object.MarshalSystem(collection) (system.go:10-31) for n collections:
+ * 0x01 | EncodeStruct(collection) | 0x00. Exact encoded lengths in d_sizes,
+ * statuses as honu_encode_sizes (HONU_ERR_INPUT for spans or lists outside
+ * their arenas). A row without HONU_HAS_COLLECTION encodes MarshalSystem(nil)
+ * = 01 00 00. */
+int32_t honu_system_sizes(honu_ctx *ctx, const honu_collection *d_rows, uint64_t var_len,
+                          const honu_acl *d_acl, uint64_t acl_len, const uint32_t *d_regions,
+                          uint64_t regions_len, const honu_index *d_index, uint64_t index_len,
+                          uint64_t n, uint64_t *d_sizes, int32_t *d_status, void *stream);
+/* Writes records at d_out + d_out_off[i] (offsets from honu_exclusive_scan of
+ * the sizes); skips records whose status is not HONU_OK. */
+int32_t honu_system_encode(honu_ctx *ctx, const honu_collection *d_rows, const uint8_t *d_var,
+                           const honu_acl *d_acl, const uint32_t *d_regions,
+                           const honu_index *d_index, uint64_t n, uint8_t *d_out,
+                           uint64_t out_cap, const uint64_t *d_out_off, int32_t *d_status,
+                           void *stream);
+/* sizes + scan (d_out_off has n+1 entries) + encode. */
+int32_t honu_system_marshal_batch(honu_ctx *ctx, const honu_collection *d_rows,
+                                  const uint8_t *d_var, uint64_t var_len, const honu_acl *d_acl,
+                                  uint64_t acl_len, const uint32_t *d_regions,
+                                  uint64_t regions_len, const honu_index *d_index,
+                                  uint64_t index_len, uint64_t n, uint8_t *d_out,
+                                  uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status,
+                                  void *stream);
+/* object.UnmarshalSystem(obj, &metadata.Collection{}) (system.go:33-45) for
+ * n records: decodes obj[1 : len-1] (the storage version byte is not checked,
+ * the trailing nil-metadata byte is not read). Rows as honu_meta decode
+ * (spans absolute in the records arena; fields of nil structs zero; a nil
+ * collection leaves a zero row). ACL entries, regions and index rows go to
+ * the tables (capacities in entries); d_status[i] is the UnmarshalSystem
+ * error, HONU_ERR_PANIC for records shorter than 2 bytes (slice bounds) and
+ * for counts Go's make() rejects. d_totals (3 u64, device): ACL entries,
+ * regions, indexes. */
+int32_t honu_system_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                                 uint64_t n, honu_collection *d_rows, int32_t *d_status,
+                                 honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
+                                 uint64_t regions_cap, honu_index *d_index, uint64_t index_cap,
+                                 uint64_t *d_totals, void *stream);
 
 /* ------------------------------------------------------------------------ */
 /* Synthetic workload (bench/test support; mirrors the reference benchmark   */

@@ -640,3 +640,442 @@ int oracle_key(const honu_meta *m, int32_t meta_status, uint8_t key[29]) {
     for (int i = 0; i < 4; i++) key[25 + i] = (uint8_t)(m->pid >> (24 - 8 * i));
     return HONU_OK;
 }
+
+/* ===================================================================== */
+/* System objects: object/system.go with metadata.Collection              */
+/* (collection.go), Index (index.go) and Field (field.go).                */
+/* ===================================================================== */
+
+/* Size() upper bounds: Field.Size field.go:38-40 (27 + len Name),
+ * Index.Size index.go:47-56 (29 + len Name + Field + Ref),
+ * Collection.Size collection.go:81-135 (115 + ...). */
+int64_t oracle_field_size(uint64_t name_len) { return 27 + (int64_t)name_len; }
+
+int64_t oracle_index_size(const honu_index *x) {
+    int64_t s = 29 + (int64_t)x->name.len;
+    if (x->has_field) s += oracle_field_size(x->field_name.len);
+    if (x->has_ref) s += oracle_field_size(x->ref_name.len);
+    return s;
+}
+
+int64_t oracle_collection_size(const honu_collection *c, const honu_acl *acl,
+                               const honu_index *idx) {
+    const int64_t scalar = MAX_VARINT_LEN32 + MAX_VARINT_LEN64;
+    int64_t s = 115 + (int64_t)c->name.len;
+    if (c->present & HONU_HAS_VERSION)
+        s += 12 + scalar + ((c->present & HONU_HAS_PARENT) ? scalar : 0);
+    s += (int64_t)c->acl_count * MAX_VARINT_LEN64;
+    for (uint64_t i = 0; i < c->acl_count; i++) s += 1 + (acl[c->acl_off + i].present ? 17 : 0);
+    s += (int64_t)c->regions_count * MAX_VARINT_LEN64;
+    s += (int64_t)c->regions_count * MAX_VARINT_LEN32;
+    if (c->present & HONU_HAS_PUBLISHER)
+        s += 52 + (int64_t)c->ip_address.len + (int64_t)c->user_agent.len;
+    if (c->present & HONU_HAS_SCHEMA) s += 25 + (int64_t)c->schema_name.len;
+    if (c->present & HONU_HAS_ENCRYPTION)
+        s += 43 + (int64_t)(c->public_key_id.len + c->encryption_key.len + c->hmac_secret.len +
+                            c->signature.len);
+    if (c->present & HONU_HAS_COMPRESSION) s += 11;
+    s += (int64_t)c->index_count * MAX_VARINT_LEN64;
+    for (uint64_t i = 0; i < c->index_count; i++) {
+        const honu_index *x = &idx[c->index_off + i];
+        s += 1 + (x->present ? oracle_index_size(x) : 0);
+    }
+    return s;
+}
+
+/* Field.Encode field.go:42-60 after its EncodeStruct flag */
+static void encode_field(owriter *w, const uint8_t *name, uint64_t name_len, uint8_t type,
+                         const uint8_t col[16]) {
+    w_frame(w, name, name_len);                      /* EncodeString(Name) */
+    w_byte(w, type);                                 /* EncodeUint8(Type) */
+    w_bytes(w, col, 16);                             /* EncodeULID(Collection) */
+}
+
+/* Collection.Encode (collection.go:137-237) preceded by its EncodeStruct flag */
+static int encode_collection(owriter *w, const honu_collection *c, const uint8_t *var,
+                             uint64_t var_len, const honu_acl *acl, uint64_t acl_len,
+                             const uint32_t *regions, uint64_t regions_len, const honu_index *idx,
+                             uint64_t idx_len) {
+    int bad = 0;
+    const uint8_t *name = span_ptr(var, var_len, c->name, &bad);
+    const uint8_t *sname = span_ptr(var, var_len, c->schema_name, &bad);
+    const uint8_t *ip = span_ptr(var, var_len, c->ip_address, &bad);
+    const uint8_t *ua = span_ptr(var, var_len, c->user_agent, &bad);
+    const uint8_t *pk = span_ptr(var, var_len, c->public_key_id, &bad);
+    const uint8_t *ek = span_ptr(var, var_len, c->encryption_key, &bad);
+    const uint8_t *hs = span_ptr(var, var_len, c->hmac_secret, &bad);
+    const uint8_t *sg = span_ptr(var, var_len, c->signature, &bad);
+    if (c->acl_count && (c->acl_off > acl_len || c->acl_count > acl_len - c->acl_off)) bad = 1;
+    if (c->regions_count &&
+        (c->regions_off > regions_len || c->regions_count > regions_len - c->regions_off))
+        bad = 1;
+    if (c->index_count && (c->index_off > idx_len || c->index_count > idx_len - c->index_off))
+        bad = 1;
+    for (uint64_t i = 0; !bad && i < c->index_count; i++) {
+        const honu_index *x = &idx[c->index_off + i];
+        if (!x->present) continue;
+        span_ptr(var, var_len, x->name, &bad);
+        if (x->has_field) span_ptr(var, var_len, x->field_name, &bad);
+        if (x->has_ref) span_ptr(var, var_len, x->ref_name, &bad);
+    }
+    if (bad) return HONU_ERR_INPUT;
+
+    w_bool(w, 1);                                    /* EncodeStruct(obj) system.go:22 */
+    w_bytes(w, c->id, 16);                           /* :139 EncodeULID(ID) */
+    w_frame(w, name, c->name.len);                   /* :144 EncodeString(Name) */
+    if (c->present & HONU_HAS_VERSION) {             /* :149 EncodeStruct(Version) */
+        w_bool(w, 1);
+        w_uvarint(w, c->pid);
+        w_uvarint(w, c->vid);
+        w_uvarint(w, c->region);
+        if (c->present & HONU_HAS_PARENT) {
+            w_bool(w, 1);
+            w_uvarint(w, c->parent_pid);
+            w_uvarint(w, c->parent_vid);
+        } else {
+            w_bool(w, 0);
+        }
+        w_bool(w, c->tombstone != 0);
+        w_time(w, c->version_created);
+    } else {
+        w_bool(w, 0);
+    }
+    w_bytes(w, c->owner, 16);                        /* :154 */
+    w_bytes(w, c->group, 16);                        /* :159 */
+    w_byte(w, c->permissions);                       /* :164 */
+    w_uvarint(w, c->acl_count);                      /* :170 EncodeUint64(len ACL) */
+    for (uint64_t i = 0; i < c->acl_count; i++) {    /* :176-181 */
+        const honu_acl *a = &acl[c->acl_off + i];
+        if (a->present) {
+            w_bool(w, 1);
+            w_bytes(w, a->client_id, 16);
+            w_byte(w, a->permissions);
+        } else {
+            w_bool(w, 0);
+        }
+    }
+    w_uvarint(w, c->regions_count);                  /* :183 WriteRegions.Encode */
+    for (uint64_t i = 0; i < c->regions_count; i++) w_uvarint(w, regions[c->regions_off + i]);
+    if (c->present & HONU_HAS_PUBLISHER) {           /* :188 */
+        w_bool(w, 1);
+        w_bytes(w, c->publisher_id, 16);
+        w_bytes(w, c->client_id, 16);
+        w_frame(w, ip, c->ip_address.len);
+        w_frame(w, ua, c->user_agent.len);
+    } else {
+        w_bool(w, 0);
+    }
+    if (c->present & HONU_HAS_SCHEMA) {              /* :193 */
+        w_bool(w, 1);
+        w_frame(w, sname, c->schema_name.len);
+        w_uvarint(w, c->schema_major);
+        w_uvarint(w, c->schema_minor);
+        w_uvarint(w, c->schema_patch);
+    } else {
+        w_bool(w, 0);
+    }
+    if (c->present & HONU_HAS_ENCRYPTION) {          /* :198 */
+        w_bool(w, 1);
+        w_frame(w, pk, c->public_key_id.len);
+        w_frame(w, ek, c->encryption_key.len);
+        w_frame(w, hs, c->hmac_secret.len);
+        w_frame(w, sg, c->signature.len);
+        w_byte(w, c->sealing_alg);
+        w_byte(w, c->encryption_alg);
+        w_byte(w, c->signature_alg);
+    } else {
+        w_bool(w, 0);
+    }
+    if (c->present & HONU_HAS_COMPRESSION) {         /* :203 */
+        w_bool(w, 1);
+        w_byte(w, c->compression_alg);
+        w_varint(w, c->compression_level);
+    } else {
+        w_bool(w, 0);
+    }
+    w_byte(w, c->flags);                             /* :208 */
+    w_uvarint(w, c->index_count);                    /* :214 EncodeUint64(len Indexes) */
+    for (uint64_t i = 0; i < c->index_count; i++) {  /* :220-225; index.go:58-86 */
+        const honu_index *x = &idx[c->index_off + i];
+        if (!x->present) {
+            w_bool(w, 0);
+            continue;
+        }
+        w_bool(w, 1);
+        w_bytes(w, x->id, 16);
+        w_frame(w, span_ptr(var, var_len, x->name, &bad), x->name.len);
+        w_byte(w, x->type);
+        if (x->has_field) {
+            w_bool(w, 1);
+            encode_field(w, span_ptr(var, var_len, x->field_name, &bad), x->field_name.len,
+                         x->field_type, x->field_collection);
+        } else {
+            w_bool(w, 0);
+        }
+        if (x->has_ref) {
+            w_bool(w, 1);
+            encode_field(w, span_ptr(var, var_len, x->ref_name, &bad), x->ref_name.len,
+                         x->ref_type, x->ref_collection);
+        } else {
+            w_bool(w, 0);
+        }
+    }
+    w_time(w, c->created);                           /* :227 */
+    w_time(w, c->modified);                          /* :232 */
+    return HONU_OK;
+}
+
+int oracle_system_marshal(const honu_collection *c, const uint8_t *var, uint64_t var_len,
+                          const honu_acl *acl, uint64_t acl_len, const uint32_t *regions,
+                          uint64_t regions_len, const honu_index *idx, uint64_t idx_len,
+                          uint8_t *out, uint64_t cap, uint64_t *out_len) {
+    *out_len = 0;
+    owriter w = {out, cap, 0};
+    w_byte(&w, HONU_STORAGE_VERSION);                /* system.go:17 EncodeUint8 */
+    if (c->present & HONU_HAS_COLLECTION) {          /* :22 EncodeStruct(obj) */
+        int st = encode_collection(&w, c, var, var_len, acl, acl_len, regions, regions_len, idx,
+                                   idx_len);
+        if (st != HONU_OK) return st;
+    } else {
+        w_bool(&w, 0);
+    }
+    w_bool(&w, 0);                                   /* :27 EncodeStruct(nil) */
+    *out_len = w.len;
+    if (out && w.len > cap) return HONU_ERR_CAPACITY;
+    return HONU_OK;
+}
+
+typedef struct {
+    honu_acl *acl_out;
+    uint64_t acl_cap, acl_n;
+    uint32_t *reg_out;
+    uint64_t reg_cap, reg_n;
+    honu_index *idx_out;
+    uint64_t idx_cap, idx_n;
+} osyslists;
+
+/* Field.Decode field.go:62-80 */
+static int decode_field(oreader *r, uint64_t base, honu_span *name, uint8_t *type,
+                        uint8_t col[16]) {
+    TRY(r_frame(r, base, name));
+    TRY(r_byte(r, type));
+    TRY(r_ulid(r, col));
+    return HONU_OK;
+}
+
+/* Collection.Decode (collection.go:240-356) after its nil flag */
+static int decode_collection_body(oreader *r, uint64_t base, honu_collection *c, osyslists *L) {
+    int b;
+    TRY(r_ulid(r, c->id));                           /* :248 */
+    TRY(r_frame(r, base, &c->name));                 /* :252 DecodeString */
+    TRY(r_bool(r, &b));                              /* :257 DecodeStruct(Version) */
+    if (b) {
+        c->present |= HONU_HAS_VERSION;
+        TRY(r_u32(r, &c->pid));
+        TRY(r_u64(r, &c->vid));
+        TRY(r_u32(r, &c->region));
+        TRY(r_bool(r, &b));
+        if (b) {
+            c->present |= HONU_HAS_PARENT;
+            TRY(r_u32(r, &c->parent_pid));
+            TRY(r_u64(r, &c->parent_vid));
+        }
+        TRY(r_bool(r, &b));
+        c->tombstone = (uint8_t)b;
+        TRY(r_i64(r, &c->version_created));
+    }
+    TRY(r_ulid(r, c->owner));                        /* :263 */
+    TRY(r_ulid(r, c->group));                        /* :267 */
+    TRY(r_byte(r, &c->permissions));                 /* :271 */
+    uint64_t nacl;
+    TRY(r_u64(r, &nacl));                            /* :277 */
+    if (nacl > 0) {                                  /* :282-293 */
+        if (nacl > GO_MAX_ALLOC / 8) return HONU_ERR_PANIC;
+        c->acl_off = L->acl_n;
+        for (uint64_t i = 0; i < nacl; i++) {
+            honu_acl a;
+            memset(&a, 0, sizeof a);
+            TRY(r_bool(r, &b));
+            if (b) {
+                a.present = 1;
+                TRY(r_ulid(r, a.client_id));
+                TRY(r_byte(r, &a.permissions));
+            }
+            if (L->acl_n < L->acl_cap) L->acl_out[L->acl_n] = a;
+            L->acl_n++;
+        }
+        c->acl_count = nacl;
+    }
+    uint64_t nreg;
+    TRY(r_u64(r, &nreg));                            /* :295 WriteRegions.Decode */
+    if (nreg > GO_MAX_ALLOC / 4) return HONU_ERR_PANIC;
+    c->present |= HONU_REGIONS_NONNIL;
+    c->regions_off = L->reg_n;
+    for (uint64_t i = 0; i < nreg; i++) {
+        uint32_t v;
+        TRY(r_u32(r, &v));
+        if (L->reg_n < L->reg_cap) L->reg_out[L->reg_n] = v;
+        L->reg_n++;
+    }
+    c->regions_count = nreg;
+    if (nreg == 0) c->regions_off = 0;
+    TRY(r_bool(r, &b));                              /* :299 DecodeStruct(Publisher) */
+    if (b) {
+        c->present |= HONU_HAS_PUBLISHER;
+        TRY(r_ulid(r, c->publisher_id));
+        TRY(r_ulid(r, c->client_id));
+        TRY(r_frame(r, base, &c->ip_address));
+        TRY(r_frame(r, base, &c->user_agent));
+    }
+    TRY(r_bool(r, &b));                              /* :305 DecodeStruct(Schema) */
+    if (b) {
+        c->present |= HONU_HAS_SCHEMA;
+        TRY(r_frame(r, base, &c->schema_name));
+        TRY(r_u32(r, &c->schema_major));
+        TRY(r_u32(r, &c->schema_minor));
+        TRY(r_u32(r, &c->schema_patch));
+    }
+    TRY(r_bool(r, &b));                              /* :311 DecodeStruct(Encryption) */
+    if (b) {
+        c->present |= HONU_HAS_ENCRYPTION;
+        TRY(r_frame(r, base, &c->public_key_id));
+        TRY(r_frame(r, base, &c->encryption_key));
+        TRY(r_frame(r, base, &c->hmac_secret));
+        TRY(r_frame(r, base, &c->signature));
+        TRY(r_byte(r, &c->sealing_alg));
+        TRY(r_byte(r, &c->encryption_alg));
+        TRY(r_byte(r, &c->signature_alg));
+    }
+    TRY(r_bool(r, &b));                              /* :317 DecodeStruct(Compression) */
+    if (b) {
+        c->present |= HONU_HAS_COMPRESSION;
+        TRY(r_byte(r, &c->compression_alg));
+        TRY(r_i64(r, &c->compression_level));
+    }
+    TRY(r_byte(r, &c->flags));                       /* :323 */
+    uint64_t nidx;
+    TRY(r_u64(r, &nidx));                            /* :329 */
+    if (nidx > 0) {                                  /* :334-345 */
+        if (nidx > GO_MAX_ALLOC / 8) return HONU_ERR_PANIC; /* make([]*Index, n) */
+        c->index_off = L->idx_n;
+        for (uint64_t i = 0; i < nidx; i++) {
+            honu_index x;
+            memset(&x, 0, sizeof x);
+            TRY(r_bool(r, &b));                      /* DecodeStruct(c.Indexes[i]) */
+            if (b) {                                 /* Index.Decode index.go:88-120 */
+                x.present = 1;
+                TRY(r_ulid(r, x.id));
+                TRY(r_frame(r, base, &x.name));
+                TRY(r_byte(r, &x.type));
+                TRY(r_bool(r, &b));                  /* DecodeStruct(o.Field) */
+                if (b) {
+                    x.has_field = 1;
+                    TRY(decode_field(r, base, &x.field_name, &x.field_type, x.field_collection));
+                }
+                TRY(r_bool(r, &b));                  /* DecodeStruct(o.Ref) */
+                if (b) {
+                    x.has_ref = 1;
+                    TRY(decode_field(r, base, &x.ref_name, &x.ref_type, x.ref_collection));
+                }
+            }
+            if (L->idx_n < L->idx_cap) L->idx_out[L->idx_n] = x;
+            L->idx_n++;
+        }
+        c->index_count = nidx;
+    }
+    TRY(r_i64(r, &c->created));                      /* :347 DecodeTime */
+    TRY(r_i64(r, &c->modified));                     /* :351 */
+    return HONU_OK;
+}
+
+int oracle_system_decode(const uint8_t *o, uint64_t len, uint64_t base, honu_collection *c,
+                         honu_acl *acl_out, uint64_t acl_cap, uint32_t *regions_out,
+                         uint64_t regions_cap, honu_index *idx_out, uint64_t idx_cap,
+                         uint64_t counts[3]) {
+    memset(c, 0, sizeof *c);
+    counts[0] = counts[1] = counts[2] = 0;
+    /* obj[1 : len(obj)-1] (system.go:40) panics for len < 2 */
+    if (len < 2) return HONU_ERR_PANIC;
+    oreader r = {o + 1, len - 2, 0};
+    osyslists L = {acl_out, acl_cap, 0, regions_out, regions_cap, 0, idx_out, idx_cap, 0};
+    int present;
+    int st = r_bool(&r, &present);                   /* DecodeStruct(v) :41 */
+    if (st == HONU_OK && present) {
+        c->present = HONU_HAS_COLLECTION;
+        st = decode_collection_body(&r, base + 1, c, &L);
+    }
+    if (st != HONU_OK) {
+        memset(c, 0, sizeof *c);
+        return st;
+    }
+    counts[0] = L.acl_n;
+    counts[1] = L.reg_n;
+    counts[2] = L.idx_n;
+    return HONU_OK;
+}
+
+int oracle_system_marshal_batch(const honu_collection *rows, const uint8_t *var, uint64_t var_len,
+                                const honu_acl *acl, uint64_t acl_len, const uint32_t *regions,
+                                uint64_t regions_len, const honu_index *idx, uint64_t idx_len,
+                                uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *out_off,
+                                int32_t *status) {
+    uint64_t pos = 0;
+    int any_cap = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t sz = 0;
+        int st = oracle_system_marshal(&rows[i], var, var_len, acl, acl_len, regions, regions_len,
+                                       idx, idx_len, NULL, 0, &sz);
+        out_off[i] = pos;
+        pos += sz;
+        if (status) status[i] = st;
+    }
+    out_off[n] = pos;
+    for (uint64_t i = 0; i < n; i++) {
+        if (status && status[i] != HONU_OK) continue;
+        uint64_t beg = out_off[i], end = out_off[i + 1];
+        if (end > out_cap) {
+            if (status) status[i] = HONU_ERR_CAPACITY;
+            any_cap = 1;
+            continue;
+        }
+        uint64_t sz;
+        int st = oracle_system_marshal(&rows[i], var, var_len, acl, acl_len, regions, regions_len,
+                                       idx, idx_len, out + beg, end - beg, &sz);
+        if (status) status[i] = st;
+    }
+    return any_cap ? HONU_ERR_CAPACITY : HONU_OK;
+}
+
+int oracle_system_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                               honu_collection *rows, int32_t *status, honu_acl *acl,
+                               uint64_t acl_cap, uint32_t *regions, uint64_t regions_cap,
+                               honu_index *idx, uint64_t idx_cap, uint64_t totals[3]) {
+    uint64_t pos[3] = {0, 0, 0};
+    int any_cap = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t beg = rec_off[i], len = rec_off[i + 1] - rec_off[i];
+        uint64_t cnt[3];
+        honu_acl *ao = acl ? acl + (pos[0] < acl_cap ? pos[0] : acl_cap) : NULL;
+        uint32_t *ro = regions ? regions + (pos[1] < regions_cap ? pos[1] : regions_cap) : NULL;
+        honu_index *xo = idx ? idx + (pos[2] < idx_cap ? pos[2] : idx_cap) : NULL;
+        uint64_t ac = acl && pos[0] < acl_cap ? acl_cap - pos[0] : 0;
+        uint64_t rc = regions && pos[1] < regions_cap ? regions_cap - pos[1] : 0;
+        uint64_t xc = idx && pos[2] < idx_cap ? idx_cap - pos[2] : 0;
+        int st = oracle_system_decode(rec + beg, len, beg, &rows[i], ao, ac, ro, rc, xo, xc, cnt);
+        if (st == HONU_OK) {
+            if (rows[i].acl_count) rows[i].acl_off = pos[0];
+            if (rows[i].regions_count) rows[i].regions_off = pos[1];
+            if (rows[i].index_count) rows[i].index_off = pos[2];
+            if (pos[0] + cnt[0] > acl_cap || pos[1] + cnt[1] > regions_cap ||
+                pos[2] + cnt[2] > idx_cap) {
+                st = HONU_ERR_CAPACITY;
+                any_cap = 1;
+            }
+            for (int k = 0; k < 3; k++) pos[k] += cnt[k];
+        }
+        status[i] = st;
+    }
+    if (totals)
+        for (int k = 0; k < 3; k++) totals[k] = pos[k];
+    return any_cap ? HONU_ERR_CAPACITY : HONU_OK;
+}

@@ -84,6 +84,33 @@ int oracle_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
 /* keys.New(oid, &Version.Scalar) (keys/keys.go:42-51) for a decoded row. */
 int oracle_key(const honu_meta *m, int32_t meta_status, uint8_t key[29]);
 
+/* System objects (object/system.go:10-45) with metadata.Collection
+ * (collection.go), Index (index.go) and Field (field.go). */
+int64_t oracle_field_size(uint64_t name_len);                /* Field.Size */
+int64_t oracle_index_size(const honu_index *x);              /* Index.Size */
+int64_t oracle_collection_size(const honu_collection *c, const honu_acl *acl,
+                               const honu_index *idx);       /* Collection.Size */
+/* MarshalSystem of one collection row (no HONU_HAS_COLLECTION: MarshalSystem(nil)) */
+int oracle_system_marshal(const honu_collection *c, const uint8_t *var, uint64_t var_len,
+                          const honu_acl *acl, uint64_t acl_len, const uint32_t *regions,
+                          uint64_t regions_len, const honu_index *idx, uint64_t idx_len,
+                          uint8_t *out, uint64_t cap, uint64_t *out_len);
+/* UnmarshalSystem(obj, &Collection{}) of one record at absolute offset base;
+ * counts = ACL entries, regions, indexes appended to the tables. */
+int oracle_system_decode(const uint8_t *o, uint64_t len, uint64_t base, honu_collection *c,
+                         honu_acl *acl_out, uint64_t acl_cap, uint32_t *regions_out,
+                         uint64_t regions_cap, honu_index *idx_out, uint64_t idx_cap,
+                         uint64_t counts[3]);
+int oracle_system_marshal_batch(const honu_collection *rows, const uint8_t *var, uint64_t var_len,
+                                const honu_acl *acl, uint64_t acl_len, const uint32_t *regions,
+                                uint64_t regions_len, const honu_index *idx, uint64_t idx_len,
+                                uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *out_off,
+                                int32_t *status);
+int oracle_system_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                               honu_collection *rows, int32_t *status, honu_acl *acl,
+                               uint64_t acl_cap, uint32_t *regions, uint64_t regions_cap,
+                               honu_index *idx, uint64_t idx_cap, uint64_t totals[3]);
+
 #ifdef __cplusplus
 }
 #endif

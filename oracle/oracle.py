@@ -39,6 +39,12 @@ def load():
         "oracle_marshal_batch": (C.c_int, [P, P, U64, P, U64, P, U64, P, P, U64, P, U64, P, P]),
         "oracle_decode_batch": (C.c_int, [P, P, U64, P, P, P, U64, P, U64, P, U64, P]),
         "oracle_key": (C.c_int, [P, I32, P]),
+        "oracle_field_size": (C.c_int64, [U64]),
+        "oracle_index_size": (C.c_int64, [P]),
+        "oracle_collection_size": (C.c_int64, [P, P, P]),
+        "oracle_system_marshal_batch": (C.c_int, [P, P, U64, P, U64, P, U64, P, U64, U64, P, U64,
+                                                  P, P]),
+        "oracle_system_decode_batch": (C.c_int, [P, P, U64, P, P, P, U64, P, U64, P, U64, P]),
     }
     for name, (res, args) in protos.items():
         fn = getattr(lib, name)
@@ -126,3 +132,58 @@ def key(row, meta_status: int):
     row = np.ascontiguousarray(row)
     st = load().oracle_key(_p(row), meta_status, out)
     return st, bytes(out)
+
+
+def system_marshal_batch(sb):
+    """MarshalSystem over a honu_amd.system.SystemHostBatch -> (out, off, status)."""
+    lib = load()
+    n = len(sb.rows)
+    out_off = np.zeros(n + 1, np.uint64)
+    status = np.zeros(n, np.int32)
+    args = (_p(sb.rows), _p(sb.var), len(sb.var), _p(sb.acl), len(sb.acl), _p(sb.regions),
+            len(sb.regions), _p(sb.index), len(sb.index), n)
+    lib.oracle_system_marshal_batch(*args, None, 0, _p(out_off), _p(status))
+    total = int(out_off[n])
+    out = np.zeros(max(total, 1), np.uint8)
+    lib.oracle_system_marshal_batch(*args, _p(out), total, _p(out_off), _p(status))
+    return out[:total], out_off, status
+
+
+def system_decode_batch(rec: np.ndarray, rec_off: np.ndarray):
+    """UnmarshalSystem(obj, &Collection{}) -> (rows, status, acl, regions, index, totals)."""
+    from honu_amd.metadata import ACL_DTYPE
+    from honu_amd.system import COLLECTION_DTYPE, INDEX_DTYPE
+    lib = load()
+    n = len(rec_off) - 1
+    rec = np.ascontiguousarray(rec, np.uint8)
+    if rec.size == 0:
+        rec = np.zeros(1, np.uint8)
+    rec_off = np.ascontiguousarray(rec_off, np.uint64)
+    nbytes = int(rec_off[-1]) if n >= 0 else 0
+    rows = np.zeros(max(n, 1), COLLECTION_DTYPE)
+    status = np.zeros(max(n, 1), np.int32)
+    acl = np.zeros(nbytes + 1, ACL_DTYPE)
+    reg = np.zeros(nbytes + 1, np.uint32)
+    idx = np.zeros(nbytes + 1, INDEX_DTYPE)
+    totals = np.zeros(3, np.uint64)
+    lib.oracle_system_decode_batch(_p(rec), _p(rec_off), n, _p(rows), _p(status), _p(acl),
+                                   len(acl), _p(reg), len(reg), _p(idx), len(idx), _p(totals))
+    return (rows[:n], status[:n], acl[: int(totals[0])], reg[: int(totals[1])],
+            idx[: int(totals[2])], totals)
+
+
+def collection_size(row, acl, index) -> int:
+    """Collection.Size() (collection.go:81-135) of a packed row."""
+    lib = load()
+    row = np.ascontiguousarray(row)
+    acl = np.ascontiguousarray(acl) if len(acl) else np.zeros(1, acl.dtype)
+    index = np.ascontiguousarray(index) if len(index) else np.zeros(1, index.dtype)
+    return lib.oracle_collection_size(_p(row), _p(acl), _p(index))
+
+
+def index_size(row) -> int:
+    return load().oracle_index_size(_p(np.ascontiguousarray(row)))
+
+
+def field_size(name_len: int) -> int:
+    return load().oracle_field_size(name_len)

@@ -31,7 +31,9 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 REGION_IDS = {
     "GCP_US_CENTRAL_1A": 2840280,
     "GCP_US_CENTRAL_1C": 2840282,
+    "GCP_US_EAST_1B": 2840291,
     "GCP_US_EAST_1C": 2840292,
+    "GCP_US_WEST_1A": 2840330,
     "GCP_US_WEST_1B": 2840331,
 }
 ENC_ALGS = {"PLAINTEXT": 0, "AES256_GCM": 1, "AES192_GCM": 2, "AES128_GCM": 3, "HMAC_SHA256": 4,
@@ -80,12 +82,8 @@ def _get(d: dict, key: str):
     return None
 
 
-def metadata_from_json(d: dict) -> Metadata:
-    m = Metadata()
-    if _get(d, "oid"):
-        m.ObjectID = ulid_parse(_get(d, "oid"))
-    if _get(d, "collection"):
-        m.CollectionID = ulid_parse(_get(d, "collection"))
+def _common_from_json(m, d: dict):
+    """Fields Metadata and Collection share, decoded as encoding/json does."""
     v = _get(d, "version")
     if v is not None:
         m.Version = Version(scalar_parse(_get(v, "scalar")), region_parse(_get(v, "region")),
@@ -96,7 +94,6 @@ def metadata_from_json(d: dict) -> Metadata:
     if s is not None:
         m.Schema = SchemaVersion(_get(s, "name") or "", _get(s, "major") or 0,
                                  _get(s, "minor") or 0, _get(s, "patch") or 0)
-    m.MIME = _get(d, "mime") or ""
     m.Owner = ulid_parse(_get(d, "owner"))
     m.Group = ulid_parse(_get(d, "group"))
     m.Permissions = _get(d, "permissions") or 0
@@ -123,6 +120,45 @@ def metadata_from_json(d: dict) -> Metadata:
     m.Flags = _get(d, "flags") or 0
     m.Created = time_parse(_get(d, "created")) if _get(d, "created") else 0
     m.Modified = time_parse(_get(d, "modified")) if _get(d, "modified") else 0
+
+
+def field_from_json(d: dict):
+    """metadata.Field (field.go:12-16); FieldType by name, upper-cased (:99-107)."""
+    from honu_amd.system import FIELD_TYPES, Field
+    t = (_get(d, "type") or "STRING").strip().upper()
+    return Field(_get(d, "name") or "", FIELD_TYPES.index(t),
+                 ulid_parse(_get(d, "collection")) if _get(d, "collection") else bytes(16))
+
+
+def index_from_json(d: dict):
+    """metadata.Index (index.go:16-22); IndexType by name, upper-cased (:122-130)."""
+    from honu_amd.system import INDEX_TYPES, Index
+    t = (_get(d, "type") or "UNKNOWN").strip().upper()
+    return Index(ulid_parse(_get(d, "id")), _get(d, "name") or "", INDEX_TYPES.index(t),
+                 field_from_json(_get(d, "field")) if _get(d, "field") is not None else None,
+                 field_from_json(_get(d, "ref")) if _get(d, "ref") is not None else None)
+
+
+def collection_from_json(d: dict):
+    """metadata.Collection (collection.go:16-33) as encoding/json fills it."""
+    from honu_amd.system import Collection
+    c = Collection()
+    c.ID = ulid_parse(_get(d, "id"))
+    c.Name = _get(d, "name") or ""
+    _common_from_json(c, d)
+    if _get(d, "indexes") is not None:
+        c.Indexes = [index_from_json(x) for x in _get(d, "indexes")]
+    return c
+
+
+def metadata_from_json(d: dict) -> Metadata:
+    m = Metadata()
+    if _get(d, "oid"):
+        m.ObjectID = ulid_parse(_get(d, "oid"))
+    if _get(d, "collection"):
+        m.CollectionID = ulid_parse(_get(d, "collection"))
+    m.MIME = _get(d, "mime") or ""
+    _common_from_json(m, d)
     return m
 
 
@@ -207,3 +243,58 @@ def py_marshal(m: Metadata, data: bytes) -> bytes:
     o += bytes([m.Flags]) + py_varint(m.Created) + py_varint(m.Modified)
     return bytes(o)
 
+
+
+def py_marshal_system(c) -> bytes:
+    """object.MarshalSystem(collection) restated directly from
+    collection.go:137-237 / index.go:58-86 / field.go:42-60 (cross-check only)."""
+    if c is None:
+        return b"\x01\x00\x00"
+    o = bytearray(b"\x01\x01") + c.ID + _frame(c.Name)
+    if c.Version is None:
+        o += b"\x00"
+    else:
+        v = c.Version
+        o += b"\x01" + py_uvarint(v.Scalar.PID) + py_uvarint(v.Scalar.VID) + py_uvarint(v.Region)
+        o += (b"\x01" + py_uvarint(v.Parent.PID) + py_uvarint(v.Parent.VID)) if v.Parent else b"\x00"
+        o += (b"\x01" if v.Tombstone else b"\x00") + py_varint(v.Created)
+    o += c.Owner + c.Group + bytes([c.Permissions])
+    acl = c.ACL or []
+    o += py_uvarint(len(acl))
+    for a in acl:
+        o += b"\x00" if a is None else b"\x01" + a.ClientID + bytes([a.Permissions])
+    reg = c.WriteRegions or []
+    o += py_uvarint(len(reg)) + b"".join(py_uvarint(r) for r in reg)
+    if c.Publisher is None:
+        o += b"\x00"
+    else:
+        p = c.Publisher
+        o += b"\x01" + p.PublisherID + p.ClientID + _frame(p.IPAddress) + _frame(p.UserAgent)
+    if c.Schema is None:
+        o += b"\x00"
+    else:
+        s = c.Schema
+        o += b"\x01" + _frame(s.Name) + py_uvarint(s.Major) + py_uvarint(s.Minor) + py_uvarint(s.Patch)
+    if c.Encryption is None:
+        o += b"\x00"
+    else:
+        e = c.Encryption
+        o += (b"\x01" + _frame(e.PublicKeyID) + _frame(e.EncryptionKey) + _frame(e.HMACSecret) +
+              _frame(e.Signature) + bytes([e.SealingAlgorithm, e.EncryptionAlgorithm,
+                                           e.SignatureAlgorithm]))
+    if c.Compression is None:
+        o += b"\x00"
+    else:
+        o += b"\x01" + bytes([c.Compression.Algorithm]) + py_varint(c.Compression.Level)
+    o += bytes([c.Flags])
+    idx = c.Indexes or []
+    o += py_uvarint(len(idx))
+    for x in idx:
+        if x is None:
+            o += b"\x00"
+            continue
+        o += b"\x01" + x.ID + _frame(x.Name) + bytes([x.Type])
+        for f in (x.Field, x.Ref):
+            o += b"\x00" if f is None else b"\x01" + _frame(f.Name) + bytes([f.Type]) + f.Collection
+    o += py_varint(c.Created) + py_varint(c.Modified) + b"\x00"
+    return bytes(o)

@@ -9,6 +9,7 @@ import pytest
 
 from honu_amd import _lib
 from honu_amd.metadata import ACL_DTYPE, INFO_DTYPE, META_DTYPE
+from honu_amd.system import COLLECTION_DTYPE, INDEX_DTYPE
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "honu_codec.h")
@@ -29,20 +30,25 @@ def test_library_exports_every_declared_symbol():
     assert set(names) == set(_lib.EXPORTS)
 
 
+STRUCTS = ((META_DTYPE, "honu_meta"), (ACL_DTYPE, "honu_acl"), (INFO_DTYPE, "honu_record_info"),
+           (COLLECTION_DTYPE, "honu_collection"), (INDEX_DTYPE, "honu_index"))
+
+
 def test_abi_self_description():
     lib = _lib.load()
-    assert lib.honu_abi_version() == 1
+    assert lib.honu_abi_version() == 2
     assert lib.honu_sizeof_meta() == META_DTYPE.itemsize == 352
     assert lib.honu_sizeof_acl() == ACL_DTYPE.itemsize == 20
     assert lib.honu_sizeof_record_info() == INFO_DTYPE.itemsize == 32
+    assert lib.honu_sizeof_collection() == COLLECTION_DTYPE.itemsize == 368
+    assert lib.honu_sizeof_index() == INDEX_DTYPE.itemsize == 112
     assert lib.honu_status_string(2).decode().startswith("object is malformed")
 
 
 def test_struct_offsets_match_numpy(tmp_path):
     """Compile offsetof() of every field with the system C compiler."""
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(){"]
-    for dt, ct in ((META_DTYPE, "honu_meta"), (ACL_DTYPE, "honu_acl"),
-                   (INFO_DTYPE, "honu_record_info")):
+    for dt, ct in STRUCTS:
         for name in dt.names:
             lines.append(f'printf("{ct}.{name} %zu\\n", offsetof({ct}, {name}));')
     lines.append("return 0;}")
@@ -52,8 +58,7 @@ def test_struct_offsets_match_numpy(tmp_path):
     subprocess.run(["gcc", "-std=c11", "-o", str(exe), str(c)], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
     got = dict(line.rsplit(" ", 1) for line in out.strip().splitlines())
-    for dt, ct in ((META_DTYPE, "honu_meta"), (ACL_DTYPE, "honu_acl"),
-                   (INFO_DTYPE, "honu_record_info")):
+    for dt, ct in STRUCTS:
         for name in dt.names:
             assert int(got[f"{ct}.{name}"]) == dt.fields[name][1], (ct, name)
 
