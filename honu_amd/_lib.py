@@ -45,11 +45,19 @@ _PROTOS = {
     "honu_decode_fill": (I32, [P, P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),
     "honu_decode_batch": (I32, [P, P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),
     "honu_decode_keys": (I32, [P, P, P, U64, P, P, P]),
+    "honu_decode_headers": (I32, [P, P, P, U64, P, P]),
     "honu_system_sizes": (I32, [P, P, U64, P, U64, P, U64, P, U64, U64, P, P, P]),
     "honu_system_encode": (I32, [P, P, P, P, P, P, U64, P, U64, P, P, P]),
     "honu_system_marshal_batch": (I32, [P, P, P, U64, P, U64, P, U64, P, U64, U64, P, U64, P, P,
                                         P]),
     "honu_system_decode_batch": (I32, [P, P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),
+    "honu_feed_create": (P, [C.c_int, U64, U64, C.c_uint32, C.POINTER(I32)]),
+    "honu_feed_destroy": (None, [P]),
+    "honu_feed_append": (I32, [P, P, U64]),
+    "honu_feed_reserve": (P, [P, U64, C.POINTER(I32)]),
+    "honu_feed_pending": (U64, [P]),
+    "honu_feed_submit": (I32, [P, C.POINTER(U64)]),
+    "honu_feed_wait": (I32, [P, U64, P]),
     "honu_gen_totals": (None, [U64, I32, U64, U64, P]),
     "honu_gen_meta": (None, [U64, I32, U64, U64, P, P, P, P, P]),
     "honu_gen_payload_host": (None, [U64, U64, U64, P, P]),

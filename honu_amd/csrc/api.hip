@@ -73,6 +73,7 @@ const char *honu_status_string(int32_t st) {
     case HONU_ERR_PANIC: return "input on which the Go reference panics";
     case HONU_ERR_CAPACITY: return "output capacity exceeded";
     case HONU_ERR_INPUT: return "input span or list outside its arena";
+    case HONU_UNPARSED: return "metadata not decoded (headers only)";
     case HONU_E_ARG: return "invalid argument";
     case HONU_E_WORKSPACE: return "batch larger than the context's reserved records";
     case HONU_E_HIP: return "HIP runtime error";
@@ -364,6 +365,16 @@ int32_t honu_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
     if (st) return st;
     return honu_decode_fill(ctx, d_rec, d_rec_off, n, d_meta, d_info, d_acl, acl_cap, d_regions,
                             regions_cap, d_data, data_cap, d_totals, stream);
+}
+
+int32_t honu_decode_headers(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                            uint64_t n, honu_record_info *d_info, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n && (!d_rec || !d_rec_off || !d_info)) return arg_fail("null pointer");
+    if (!aligned(d_info, 8)) return arg_fail("record info must be 8-byte aligned");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_decode_headers(d_rec, d_rec_off, n, d_info, (hipStream_t)stream));
+    return HONU_OK;
 }
 
 int32_t honu_decode_keys(honu_ctx *ctx, const honu_meta *d_meta, const honu_record_info *d_info,

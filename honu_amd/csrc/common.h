@@ -217,6 +217,18 @@ HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ s
 }
 
 // ------------------------------------------------------------------------
+// honu_record_info as four explicit 8-byte stores (padding bytes included:
+// a struct copy may leave them unwritten, and rows are compared bytewise)
+// ------------------------------------------------------------------------
+HONU_DEV void store_info(honu_record_info *p, const honu_record_info &v) {
+    uint64_t *q = reinterpret_cast<uint64_t *>(p);
+    q[0] = v.data_off;
+    q[1] = v.data_len;
+    q[2] = (uint64_t)(uint32_t)v.data_status | ((uint64_t)(uint32_t)v.meta_status << 32);
+    q[3] = (uint64_t)v.storage_version | ((uint64_t)v.tombstone << 8);
+}
+
+// ------------------------------------------------------------------------
 // synthetic payload bytes (shared by host generator and device fill)
 // ------------------------------------------------------------------------
 HONU_HD uint64_t splitmix64(uint64_t x) {

@@ -353,7 +353,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse(
             inf.tombstone = (v1 && d == 0) ? 1 : 0;  // Tombstone :103-112
 #pragma unroll
             for (int i = 0; i < 6; i++) inf._pad[i] = 0;
-            info[r] = inf;
+            store_info(info + r, inf);
             scratch[r] = DecodeScratch{acl_pos, reg_pos, data_off, end};
             counts[3 * r + 0] = nacl;
             counts[3 * r + 1] = nreg;

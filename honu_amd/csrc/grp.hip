@@ -784,7 +784,7 @@ HONU_DEV void k_decode_parse_grp_one(uint64_t i, uint8_t *smem, const uint8_t *_
         inf.tombstone = (v1 && d == 0) ? 1 : 0;  // Tombstone :103-112
 #pragma unroll
         for (int k = 0; k < 6; k++) inf._pad[k] = 0;
-        info[i] = inf;
+        store_info(info + i, inf);
         scratch[i] = DecodeScratch{acl_pos, reg_pos, data_off, end};
         counts[3 * i + 0] = nacl;
         counts[3 * i + 1] = nreg;

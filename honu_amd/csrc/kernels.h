@@ -154,6 +154,9 @@ hipError_t launch_system_fill(const uint8_t *rec, uint64_t n, honu_collection *r
                               uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap, honu_index *idx,
                               uint64_t idx_cap, hipStream_t s);
 
+hipError_t launch_decode_headers(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                                 honu_record_info *info, hipStream_t s);
+
 // Exclusive scan of K interleaved u64 columns: out[i*K+c] = sum_{j<i} in[j*K+c];
 // totals[c] = full sum. `partials` needs scan_partials_len(n, K) u64.
 uint64_t scan_partials_len(uint64_t n, int K);

@@ -200,7 +200,7 @@ done:
     inf.tombstone = (v1 && d == 0) ? 1 : 0;  // Tombstone :103-112
 #pragma unroll
     for (int k = 0; k < 6; k++) inf._pad[k] = 0;
-    info[i] = inf;
+    store_info(info + i, inf);
     scratch[i] = DecodeScratch{acl_pos, reg_pos, data_off, end};
     counts[3 * i + 0] = nacl;
     counts[3 * i + 1] = nreg;
@@ -607,6 +607,63 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
 
 #undef TRY
 #undef OFF
+
+// ------------------------------------------------------------------------
+// headers only: StorageVersion, Data, Tombstone (object.go:47-52,85-134)
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(HONU_BLOCK) void k_decode_headers(
+    const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
+    honu_record_info *__restrict__ info) {
+    for (uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * HONU_BLOCK) {
+        const uint64_t beg = rec_off[i], end = rec_off[i + 1];
+        const uint64_t len = end - beg;
+        uint32_t ver = 0;
+        int64_t d = -1, b = -1;
+        if (len) {
+            uint64_t lo, hi;
+            lane_fetch16(rec, beg, end, lo, hi);
+            ver = (uint32_t)(lo & 0xFF);
+            if (len >= 3) {  // dataLength: Uvarint(o[1 : min(11, len-1)])
+                const uint32_t wl = (uint32_t)(len - 2 < 10 ? len - 2 : 10);
+                uint64_t x;
+                const uint32_t k = uvarint_window((lo >> 8) | (hi << 56), hi >> 8, wl, x);
+                if (k) {
+                    d = (int64_t)x;
+                    b = k;
+                }
+            }
+        }
+        const bool v1 = ver == HONU_STORAGE_VERSION;
+        honu_record_info inf;
+        inf.data_off = 0;
+        inf.data_len = 0;
+        if (!v1) inf.data_status = HONU_ERR_BAD_VERSION;
+        else if (d < 0) inf.data_status = HONU_ERR_MALFORMED;
+        else if (d == 0) inf.data_status = HONU_OK;
+        else if ((uint64_t)d > len - 1 - (uint64_t)b) inf.data_status = HONU_ERR_PANIC;
+        else {
+            inf.data_status = HONU_OK;
+            inf.data_off = beg + 1 + (uint64_t)b;
+            inf.data_len = (uint64_t)d;
+        }
+        inf.meta_status = HONU_UNPARSED;
+        inf.storage_version = (uint8_t)ver;
+        inf.tombstone = (v1 && d == 0) ? 1 : 0;
+#pragma unroll
+        for (int k = 0; k < 6; k++) inf._pad[k] = 0;
+        store_info(info + i, inf);
+    }
+}
+
+hipError_t launch_decode_headers(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                                 honu_record_info *info, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t b = (n + HONU_BLOCK - 1) / HONU_BLOCK;
+    hipLaunchKernelGGL(k_decode_headers, dim3((unsigned)(b > 65536 ? 65536 : b)), dim3(HONU_BLOCK),
+                       0, s, rec, rec_off, n, info);
+    return hipGetLastError();
+}
 
 static dim3 lane_grid(uint64_t n, int cap) {
     const uint64_t b = (n + HONU_BLOCK - 1) / HONU_BLOCK;

@@ -479,7 +479,9 @@ HONU_DEV void system_fill_one(uint64_t i, const uint8_t *__restrict__ rec,
             e[3] = (uint32_t)(hi >> 32);
             e[4] = u | (1u << 8);
         }
-        acl[ao + k] = a;
+        uint32_t *dst = reinterpret_cast<uint32_t *>(acl + ao + k);
+#pragma unroll
+        for (int j = 0; j < 5; j++) dst[j] = e[j];
     }
     D.p = sc.regions_pos;
     for (uint64_t k = 0; k < nr; k++) {
@@ -513,7 +515,9 @@ HONU_DEV void system_fill_one(uint64_t i, const uint8_t *__restrict__ rec,
                 fill_field(D, x.ref_name, x.ref_type, x.ref_collection);
             }
         }
-        idx[xo + k] = x;
+        uint32_t *dst = reinterpret_cast<uint32_t *>(idx + xo + k);
+#pragma unroll
+        for (int j = 0; j < (int)(sizeof(honu_index) / 4); j++) dst[j] = w[j];
     }
 }
 

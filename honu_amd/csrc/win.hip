@@ -381,7 +381,7 @@ HONU_DEV void parse_win_one(
     inf.tombstone = (v1 && d == 0) ? 1 : 0;  // Tombstone :103-112
 #pragma unroll
     for (int k = 0; k < 6; k++) inf._pad[k] = 0;
-    info[i] = inf;
+    store_info(info + i, inf);
     scratch[i] = DecodeScratch{acl_pos, reg_pos, data_off, end};
     counts[3 * i + 0] = nacl;
     counts[3 * i + 1] = nreg;

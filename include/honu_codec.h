@@ -64,6 +64,7 @@ typedef enum honu_status {
                                     nil *Metadata in Marshal metadata.go:66) */
     HONU_ERR_CAPACITY = 9,       /* an output arena/table was too small (ABI only) */
     HONU_ERR_INPUT = 10,         /* an encode input span/list points outside its arena (ABI only) */
+    HONU_UNPARSED = 11,          /* meta_status of honu_decode_headers: Metadata() not evaluated */
     /* call-level errors (returned, never written per record) */
     HONU_E_ARG = -1,
     HONU_E_WORKSPACE = -2,       /* n exceeds the context's reserved record count */
@@ -303,6 +304,13 @@ int32_t honu_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
                           uint64_t regions_cap, uint8_t *d_data, uint64_t data_cap,
                           uint64_t *d_totals, void *stream);
 
+/* Object.StorageVersion() / Data() / Tombstone() (object.go:47-52,85-112)
+ * without Metadata(): every honu_record_info field but meta_status, which is
+ * HONU_UNPARSED. Reads only each record's header (version byte + the
+ * dataLength varint): the Collection.Exists path (collection.go:55-65). */
+int32_t honu_decode_headers(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                            uint64_t n, honu_record_info *d_info, void *stream);
+
 /* Object.Key() (object.go:57-64 -> keys.New, keys/keys.go:42-51) for every
  * decoded record: 0x01 | ObjectID | BE64(VID) | BE32(PID), 29 bytes per
  * record at d_keys + 29*i. d_key_status[i] = meta_status, or HONU_ERR_PANIC
@@ -429,6 +437,60 @@ int32_t honu_system_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint
                                  honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
                                  uint64_t regions_cap, honu_index *d_index, uint64_t index_cap,
                                  uint64_t *d_totals, void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* Read feed: the local-storage read path (iterator/cursor.go:31-38 copies    */
+/* each bbolt value; Collection.Exists, collection.go:55-65, asks Tombstone). */
+/* Records are appended into pinned host memory; each submitted batch is      */
+/* copied to the device, decoded (zero copy) and keyed on its own stream      */
+/* while the next batch fills: two slots, so the H2D copy, the kernels and    */
+/* the D2H copies of one batch overlap the host filling the other.            */
+/* ------------------------------------------------------------------------ */
+typedef struct honu_feed honu_feed;
+
+enum {
+    HONU_FEED_HEADERS = 1u << 0  /* StorageVersion/Data/Tombstone only (honu_decode_headers) */
+};
+
+/* Host views of a decoded batch, valid until the next append/reserve into the
+ * same slot (one more submit). Spans in meta rows and info.data_off are
+ * absolute offsets into `records` (the batch's pinned arena), so Data() is the
+ * subslice records[data_off : data_off + data_len], as in the reference. */
+typedef struct honu_feed_result {
+    uint64_t n;                       /* records in the batch */
+    const uint8_t *records;           /* pinned arena holding the batch's records */
+    const uint64_t *rec_off;          /* n + 1 offsets into records */
+    const honu_meta *meta;            /* n rows (NULL with HONU_FEED_HEADERS) */
+    const honu_record_info *info;     /* n */
+    const honu_acl *acl;              /* acl_n entries */
+    uint64_t acl_n;
+    const uint32_t *regions;          /* regions_n entries */
+    uint64_t regions_n;
+    const uint8_t *keys;              /* 29 * n bytes, Object.Key() (NULL with HEADERS) */
+    const int32_t *key_status;        /* n */
+} honu_feed_result;
+
+/* A feed with two slots of batch_records records / batch_bytes bytes each.
+ * The decoded ACL / region tables hold batch_bytes/8 + 1024 and
+ * batch_bytes/4 + 1024 entries per batch; a batch that needs more reports
+ * HONU_ERR_CAPACITY in the meta_status of the records that did not fit. */
+honu_feed *honu_feed_create(int device, uint64_t batch_records, uint64_t batch_bytes,
+                            uint32_t flags, int32_t *err);
+void honu_feed_destroy(honu_feed *feed);
+/* Copy one record into the current batch: HONU_ERR_CAPACITY when it does not
+ * fit (submit, then append again), HONU_E_ARG when the slot still holds a
+ * batch that was submitted but not waited for. */
+int32_t honu_feed_append(honu_feed *feed, const uint8_t *rec, uint64_t len);
+/* Reserve len bytes for the next record in pinned memory and return the
+ * pointer (the caller writes the record there), or NULL with *err set. */
+uint8_t *honu_feed_reserve(honu_feed *feed, uint64_t len, int32_t *err);
+/* Records in the current (filling) batch. */
+uint64_t honu_feed_pending(const honu_feed *feed);
+/* Start decoding the current batch (asynchronous); *ticket identifies it.
+ * The other slot becomes the filling one. */
+int32_t honu_feed_submit(honu_feed *feed, uint64_t *ticket);
+/* Wait for a submitted batch and describe its results. */
+int32_t honu_feed_wait(honu_feed *feed, uint64_t ticket, honu_feed_result *out);
 
 /* ------------------------------------------------------------------------ */
 /* Synthetic workload (bench/test support; mirrors the reference benchmark   */
