@@ -65,6 +65,8 @@ def parse_args():
                         "beside them (0 = no cap; -1 = auto: 2 when records average > 64 KiB, "
                         "where the copies dominate, else no cap)")
     p.add_argument("--copy-prio", type=int, default=1, help="copy stream gets high priority")
+    p.add_argument("--copy-blocks", type=int, default=0,
+                   help="workgroups per CU of the payload copy engine (0 = library default)")
     return p.parse_args()
 
 
@@ -152,6 +154,10 @@ class Bench:
         if lane_blocks < 0:
             lane_blocks = 2 if self.total_rec_bytes / N > 65536 else 0
         self.lane_blocks = 0 if args.serial else lane_blocks
+        for sl in self.slots:
+            if args.copy_blocks:
+                _lib.check(self.lib.honu_ctx_set_param(sl.codec.ctx, b"copy_blocks",
+                                                       args.copy_blocks * ncu), "param")
         if not args.serial:
             for sl in self.slots:
                 if args.meta_blocks:
@@ -486,6 +492,7 @@ def main():
             "streams": 1 if args.serial else 2,
             "meta_blocks_per_cu": 8 if (args.serial or not args.meta_blocks) else args.meta_blocks,
             "lane_blocks_per_cu": bench.lane_blocks or None,
+            "copy_blocks_per_cu": args.copy_blocks or 2,
         },
         "records_per_s": total_records / step_s,
         "roofline": {
