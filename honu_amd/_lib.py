@@ -11,7 +11,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhonu_codec.so")
+LIB_PATH = os.environ.get("HONU_LIB_PATH") or os.path.join(_HERE, "libhonu_codec.so")  # override: A/B builds
 
 _lib = None
 

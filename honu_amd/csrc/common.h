@@ -171,23 +171,19 @@ HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ s
     const uint64_t d0 = (uint64_t)dst;
     uint64_t head = (16u - (d0 & 15u)) & 15u;
     if (head > n) head = n;
-    const uint64_t chunks = (n - head) >> 4;
-    const uint64_t tail = (n - head) & 15u;
-    const uint64_t t0 = head + (chunks << 4);
-    // The edge bytes are loaded up front and stored after the chunk loop, so
-    // their round trips overlap the chunk loads instead of preceding and
-    // following them (a short segment then costs one round trip, not three).
-    uint8_t hb = 0, tb = 0;
-    if (lane < head) hb = src[lane];
-    if (lane < tail) tb = src[t0 + lane];
-    u32x4 *__restrict__ d4 = reinterpret_cast<u32x4 *>(dst + head);
-    const uint8_t *s1 = src + head;
-    const uint32_t p = (uint32_t)((uint64_t)s1 & 15u);
+    if (head && lane < head) dst[lane] = src[lane];
+    dst += head;
+    src += head;
+    n -= head;
+    const uint64_t chunks = n >> 4;
+    const uint64_t tail = n & 15u;
+    u32x4 *__restrict__ d4 = reinterpret_cast<u32x4 *>(dst);
+    const uint32_t p = (uint32_t)((uint64_t)src & 15u);
     // Every iteration issues all its loads before any store, with per-chunk
     // predication instead of a serial remainder loop, so a short segment costs
     // one round trip, not one per 1 KiB.
     if (p == 0) {
-        const u32x4 *__restrict__ s4 = reinterpret_cast<const u32x4 *>(s1);
+        const u32x4 *__restrict__ s4 = reinterpret_cast<const u32x4 *>(src);
         for (uint64_t c = lane; c < chunks; c += UNROLL * HONU_WAVE) {
             u32x4 v[UNROLL];
 #pragma unroll
@@ -198,7 +194,7 @@ HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ s
                 if (c + u * HONU_WAVE < chunks) st16<NT>(&d4[c + u * HONU_WAVE], v[u]);
         }
     } else {
-        const u32x4 *__restrict__ s4 = reinterpret_cast<const u32x4 *>(s1 - p);
+        const u32x4 *__restrict__ s4 = reinterpret_cast<const u32x4 *>(src - p);
         for (uint64_t c = lane; c < chunks; c += UNROLL * HONU_WAVE) {
             u32x4 lo[UNROLL], hi[UNROLL];
 #pragma unroll
@@ -214,8 +210,10 @@ HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ s
                     st16<NT>(&d4[c + u * HONU_WAVE], funnel16(lo[u], hi[u], p));
         }
     }
-    if (lane < head) dst[lane] = hb;
-    if (lane < tail) dst[t0 + lane] = tb;
+    if (tail) {
+        const uint64_t t0 = chunks << 4;
+        if (lane < tail) dst[t0 + lane] = src[t0 + lane];
+    }
 }
 
 // ------------------------------------------------------------------------

@@ -67,38 +67,6 @@ struct DecodeSegments {
 
 #define SMALL_SEG_WAVES_FACTOR 4
 
-// Segment i clipped to the wave's logical range [lo, hi): live = false once
-// the segments start at or past hi (or i >= n); len = 0 for an empty or
-// skipped piece.
-struct Piece {
-    const uint8_t *src;
-    uint8_t *dst;
-    uint64_t len;
-    bool live;
-};
-
-template <class Seg>
-HONU_DEV Piece piece(const Seg &seg, uint64_t i, uint64_t n, uint64_t lo, uint64_t hi) {
-    Piece p{nullptr, nullptr, 0, false};
-    if (i >= n) return p;
-    const uint64_t s = seg.start(i);
-    if (s >= hi) return p;
-    p.live = true;
-    uint64_t len;
-    const uint8_t *src;
-    uint8_t *dst;
-    if (!seg.get(i, len, src, dst)) return p;
-    const uint64_t x = s > lo ? s : lo;
-    const uint64_t e = s + len;
-    const uint64_t y = e < hi ? e : hi;
-    if (x < y) {
-        p.src = src + (x - s);
-        p.dst = dst + (x - s);
-        p.len = y - x;
-    }
-    return p;
-}
-
 template <class Seg, int UNROLL, bool NT>
 __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t n,
                                                                const uint64_t *__restrict__ total_p) {
@@ -121,21 +89,18 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t 
         if (seg.start(mid) <= lo) a = mid;
         else b = mid;
     }
-    // Descriptors are fetched 64 segments at a time, one per lane (vector
-    // loads: one round trip per 64 segments instead of a chain of dependent
-    // scalar loads per segment), then handed to the whole wave by readlane.
-    for (uint64_t i0 = a; i0 < n; i0 += HONU_WAVE) {
-        const Piece pl = piece(seg, i0 + lane_id(), n, lo, hi);
-        const uint64_t live = __builtin_amdgcn_ballot_w64(pl.live);  // a prefix of the lanes
-        const uint32_t cnt = (uint32_t)__builtin_popcountll(live);
-        for (uint32_t k = 0; k < cnt; k++) {
-            const uint64_t len = readlane64(pl.len, k);
-            if (len)
-                wave_copy<UNROLL, NT>(reinterpret_cast<uint8_t *>(readlane64((uint64_t)pl.dst, k)),
-                                      reinterpret_cast<const uint8_t *>(readlane64((uint64_t)pl.src, k)),
-                                      len);
-        }
-        if (cnt < HONU_WAVE) break;
+    for (uint64_t i = a; i < n; i++) {
+        const uint64_t s = seg.start(i);
+        if (s >= hi) break;
+        uint64_t len;
+        const uint8_t *src;
+        uint8_t *dst;
+        if (!seg.get(i, len, src, dst)) continue;
+        const uint64_t x = s > lo ? s : lo;
+        const uint64_t e = s + len;
+        const uint64_t y = e < hi ? e : hi;
+        if (x < y)
+            wave_copy<UNROLL, NT>(dst + (x - s), src + (x - s), y - x);
     }
 }
 
