@@ -54,10 +54,18 @@ _PROTOS = {
     "honu_feed_create": (P, [C.c_int, U64, U64, C.c_uint32, C.POINTER(I32)]),
     "honu_feed_destroy": (None, [P]),
     "honu_feed_append": (I32, [P, P, U64]),
+    "honu_feed_append_batch": (I32, [P, P, P, U64, C.POINTER(U64)]),
     "honu_feed_reserve": (P, [P, U64, C.POINTER(I32)]),
     "honu_feed_pending": (U64, [P]),
     "honu_feed_submit": (I32, [P, C.POINTER(U64)]),
     "honu_feed_wait": (I32, [P, U64, P]),
+    "honu_put_feed_create": (P, [C.c_int, U64, U64, C.POINTER(I32)]),
+    "honu_put_feed_destroy": (None, [P]),
+    "honu_put_feed_append": (I32, [P, P, P, U64, P, U64, P, U64, P, U64]),
+    "honu_put_feed_append_batch": (I32, [P, P, U64, P, U64, P, U64, P, U64, P, P, C.POINTER(U64)]),
+    "honu_put_feed_pending": (U64, [P]),
+    "honu_put_feed_submit": (I32, [P, C.POINTER(U64)]),
+    "honu_put_feed_wait": (I32, [P, U64, P]),
     "honu_gen_totals": (None, [U64, I32, U64, U64, P]),
     "honu_gen_meta": (None, [U64, I32, U64, U64, P, P, P, P, P]),
     "honu_gen_payload_host": (None, [U64, U64, U64, P, P]),

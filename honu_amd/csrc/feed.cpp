@@ -197,6 +197,19 @@ int32_t honu_feed_append(honu_feed *f, const uint8_t *rec, uint64_t len) {
     return HONU_OK;
 }
 
+int32_t honu_feed_append_batch(honu_feed *f, const uint8_t *arena, const uint64_t *off, uint64_t n,
+                               uint64_t *appended) {
+    if (!f || (n && (!arena || !off)) || !appended) return HONU_E_ARG;
+    *appended = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (off[i + 1] < off[i]) return HONU_E_ARG;
+        const int32_t st = honu_feed_append(f, arena + off[i], off[i + 1] - off[i]);
+        if (st != HONU_OK) return st;
+        *appended = i + 1;
+    }
+    return HONU_OK;
+}
+
 uint64_t honu_feed_pending(const honu_feed *f) {
     if (!f) return 0;
     const Slot &s = f->slot[f->cur];

@@ -73,6 +73,18 @@ class RecordFeed:
             _lib.check(st, "honu_feed_append")
         return st
 
+    def append_batch(self, arena: np.ndarray, off: np.ndarray, first: int = 0):
+        """Append records first.. of a CSR arena until the batch is full.
+        Returns (status, records appended)."""
+        n = len(off) - 1 - first
+        got = C.c_uint64(0)
+        st = self.lib.honu_feed_append_batch(self.feed, arena.ctypes.data,
+                                             off[first:].ctypes.data if n else None, n,
+                                             C.byref(got))
+        if st not in (0, 9):
+            _lib.check(st, "honu_feed_append_batch")
+        return st, got.value
+
     @property
     def pending(self) -> int:
         return self.lib.honu_feed_pending(self.feed)
@@ -96,3 +108,94 @@ class RecordFeed:
             None if hdr else _view(r.regions, r.regions_n, np.uint32),
             None if hdr else _view(r.keys, 29 * n, np.uint8).reshape(n, 29),
             None if hdr else _view(r.key_status, n, np.int32))
+
+
+# --------------------------------------------------------------------------
+# Write feed (include/honu_codec.h, "Write feed"): object.Marshal for a
+# store's Put path, batched through pinned memory and the GPU encoder.
+# --------------------------------------------------------------------------
+class _PutResult(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("records", C.c_void_p), ("rec_off", C.c_void_p),
+                ("status", C.c_void_p)]
+
+
+@dataclass
+class PutResult:
+    records: np.ndarray   # encoded records back to back (views of pinned memory)
+    rec_off: np.ndarray   # n + 1
+    status: np.ndarray    # n, honu_status per record
+
+    def objects(self):
+        """Marshal's result per record: bytes, or the status code on failure."""
+        return [int(s) if s else self.records[int(self.rec_off[i]):int(self.rec_off[i + 1])].tobytes()
+                for i, s in enumerate(self.status)]
+
+
+class PutFeed:
+    """object.Marshal(meta, data) over batches: append() one record (a
+    metadata.Metadata mirror or None + payload bytes or None), append_batch()
+    a whole host batch (HostBatch), submit() a batch, wait() for its records.
+    Results are views of pinned buffers, valid until the slot is refilled."""
+
+    def __init__(self, device: int = 0, batch_records: int = 1 << 16, batch_bytes: int = 64 << 20):
+        self.lib = _lib.load()
+        err = _lib.I32(0)
+        self.feed = self.lib.honu_put_feed_create(device, batch_records, batch_bytes, C.byref(err))
+        if not self.feed:
+            _lib.check(err.value or -4, "honu_put_feed_create")
+
+    def close(self):
+        if getattr(self, "feed", None):
+            self.lib.honu_put_feed_destroy(self.feed)
+            self.feed = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def append(self, meta, data: Optional[bytes]) -> int:
+        """0 on success, HONU_ERR_CAPACITY (9) when the batch is full."""
+        from .metadata import pack_batch
+        hb = pack_batch([meta], [data])
+        d = bytes(data) if data else b""
+        st = self.lib.honu_put_feed_append(
+            self.feed, hb.meta.ctypes.data, hb.var.ctypes.data, len(hb.var),
+            hb.acl.ctypes.data if len(hb.acl) else None, len(hb.acl),
+            hb.regions.ctypes.data if len(hb.regions) else None, len(hb.regions),
+            d or None, len(d))
+        if st not in (0, 9):
+            _lib.check(st, "honu_put_feed_append")
+        return st
+
+    def append_batch(self, hb, first: int = 0):
+        """Append records first.. of a HostBatch until the batch is full.
+        Returns (status, records appended)."""
+        n = len(hb) - first
+        got = C.c_uint64(0)
+        st = self.lib.honu_put_feed_append_batch(
+            self.feed, hb.meta[first:].ctypes.data if n else None, n,
+            hb.var.ctypes.data, len(hb.var), hb.acl.ctypes.data if len(hb.acl) else None,
+            len(hb.acl), hb.regions.ctypes.data if len(hb.regions) else None, len(hb.regions),
+            hb.payload.ctypes.data, hb.payload_off[first:].ctypes.data, C.byref(got))
+        if st not in (0, 9):
+            _lib.check(st, "honu_put_feed_append_batch")
+        return st, got.value
+
+    @property
+    def pending(self) -> int:
+        return self.lib.honu_put_feed_pending(self.feed)
+
+    def submit(self) -> int:
+        t = C.c_uint64(0)
+        _lib.check(self.lib.honu_put_feed_submit(self.feed, C.byref(t)), "honu_put_feed_submit")
+        return t.value
+
+    def wait(self, ticket: int) -> PutResult:
+        r = _PutResult()
+        _lib.check(self.lib.honu_put_feed_wait(self.feed, ticket, C.byref(r)), "honu_put_feed_wait")
+        n = r.n
+        off = _view(r.rec_off, n + 1, np.uint64)
+        return PutResult(_view(r.records, int(off[n]) if n else 0, np.uint8), off,
+                         _view(r.status, n, np.int32))

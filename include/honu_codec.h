@@ -481,6 +481,11 @@ void honu_feed_destroy(honu_feed *feed);
  * fit (submit, then append again), HONU_E_ARG when the slot still holds a
  * batch that was submitted but not waited for. */
 int32_t honu_feed_append(honu_feed *feed, const uint8_t *rec, uint64_t len);
+/* honu_feed_append for records 0..n-1 of a host CSR arena (record i =
+ * arena[off[i], off[i+1]): a cursor page), stopping at the first record that
+ * does not fit; *appended = records taken. */
+int32_t honu_feed_append_batch(honu_feed *feed, const uint8_t *arena, const uint64_t *off,
+                               uint64_t n, uint64_t *appended);
 /* Reserve len bytes for the next record in pinned memory and return the
  * pointer (the caller writes the record there), or NULL with *err set. */
 uint8_t *honu_feed_reserve(honu_feed *feed, uint64_t len, int32_t *err);
@@ -491,6 +496,57 @@ uint64_t honu_feed_pending(const honu_feed *feed);
 int32_t honu_feed_submit(honu_feed *feed, uint64_t *ticket);
 /* Wait for a submitted batch and describe its results. */
 int32_t honu_feed_wait(honu_feed *feed, uint64_t ticket, honu_feed_result *out);
+
+/* ------------------------------------------------------------------------ */
+/* Write feed: the local-storage write path (a store Put marshals one record */
+/* per call today: object.Marshal, object.go:24-45, from store.go:226,530).  */
+/* Records (row + the bytes it references + payload) are appended into      */
+/* pinned memory; each submitted batch is copied to the device, marshalled   */
+/* and copied back on its own stream while the next batch fills (two slots). */
+/* ------------------------------------------------------------------------ */
+typedef struct honu_put_feed honu_put_feed;
+
+/* Host views of a marshalled batch, valid until the slot is refilled (one
+ * more submit). Record i is records[rec_off[i], rec_off[i+1]) when
+ * status[i] == HONU_OK (Marshal's []byte); a failed record has an empty range
+ * and its error (HONU_ERR_PANIC for Marshal(nil, ...)). */
+typedef struct honu_put_result {
+    uint64_t n;
+    const uint8_t *records;
+    const uint64_t *rec_off;  /* n + 1 */
+    const int32_t *status;    /* n */
+} honu_put_result;
+
+/* A feed with two slots of batch_records records each; batch_bytes bounds a
+ * batch's input bytes: the bytes its rows' spans reference + payloads + 20
+ * per ACL entry + 4 per region. */
+honu_put_feed *honu_put_feed_create(int device, uint64_t batch_records, uint64_t batch_bytes,
+                                    int32_t *err);
+void honu_put_feed_destroy(honu_put_feed *feed);
+/* Append object.Marshal(meta, data) for one record. `row` is the record's
+ * honu_meta: its spans index var[0, var_len), acl_off/acl_count index
+ * acl[0, acl_len), regions_off/regions_count index regions[0, regions_len)
+ * (a caller may pass whole batch tables or the record's own). Only the bytes
+ * and entries the row references are copied (spans of absent sub-structs are
+ * ignored). HONU_ERR_CAPACITY: the batch is full (submit, then append again);
+ * HONU_ERR_INPUT: a span or list lies outside its array (nothing appended);
+ * HONU_E_ARG: the filling slot still holds a batch that was not waited for.
+ * data == NULL with data_len == 0 is a nil payload (a tombstone). */
+int32_t honu_put_feed_append(honu_put_feed *feed, const honu_meta *row, const uint8_t *var,
+                             uint64_t var_len, const honu_acl *acl, uint64_t acl_len,
+                             const uint32_t *regions, uint64_t regions_len, const uint8_t *data,
+                             uint64_t data_len);
+/* honu_put_feed_append for records 0..n-1 of a host CSR batch (payload i =
+ * payload[payload_off[i], payload_off[i+1])), stopping at the first record
+ * that does not go in; *appended = records taken. */
+int32_t honu_put_feed_append_batch(honu_put_feed *feed, const honu_meta *rows, uint64_t n,
+                                   const uint8_t *var, uint64_t var_len, const honu_acl *acl,
+                                   uint64_t acl_len, const uint32_t *regions, uint64_t regions_len,
+                                   const uint8_t *payload, const uint64_t *payload_off,
+                                   uint64_t *appended);
+uint64_t honu_put_feed_pending(const honu_put_feed *feed);
+int32_t honu_put_feed_submit(honu_put_feed *feed, uint64_t *ticket);
+int32_t honu_put_feed_wait(honu_put_feed *feed, uint64_t ticket, honu_put_result *out);
 
 /* ------------------------------------------------------------------------ */
 /* Synthetic workload (bench/test support; mirrors the reference benchmark   */
