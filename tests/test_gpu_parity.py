@@ -367,3 +367,40 @@ def test_copy_engine_parity(oracle_lib, copy_variant, lens):
         assert_decode_equal(oracle_lib, c, oout, ooff, materialize=True)
     finally:
         c.close()
+
+
+def test_payload_length_varint_boundaries(oracle_lib):
+    """Payload lengths at every uvarint-length boundary of the header
+    (object.go:35: 1 -> 5 bytes of length), up to a 256 MiB + 5 B payload:
+    encoded bytes, offsets, the Data() descriptors and the materialised
+    payloads are bit-exact; digests cover the big records."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    lens = [0, 1, 127, 128, 16383, 16384, (1 << 21) - 1, 1 << 21, (1 << 28) - 1, (1 << 28) + 5]
+    n = len(lens)
+    base = gen_host_batch(13, "small", 0, n)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    rng = np.random.default_rng(13)
+    pay = rng.integers(0, 256, int(off[-1]) + 1, dtype=np.uint8)
+    from honu_amd.metadata import HostBatch
+    hb = HostBatch(base.meta, base.var, base.acl, base.regions, pay, off)
+    c = hobj.Codec(0, n)
+    try:
+        out, goff, st = gpu_marshal(c, hb)
+        oout, ooff, ost = oracle_lib.marshal_batch(hb)
+        assert np.array_equal(st, ost) and (st == 0).all() and np.array_equal(goff, ooff)
+        assert out.tobytes() == oout.tobytes()
+        for i, ln in enumerate(lens):  # header: 01 | uvarint(len)
+            r = out[int(goff[i]):int(goff[i + 1])]
+            assert r[0] == 1 and bytes(r[1:1 + py_uvarint_len(ln)]) == py_uvarint(ln)
+        meta, info, acl, reg, data = assert_decode_equal(oracle_lib, c, oout, ooff, materialize=True)
+        assert (info["meta_status"] == 0).all() and (info["data_status"] == 0).all()
+        assert list(info["data_len"]) == lens
+        assert list(info["tombstone"]) == [1] + [0] * (n - 1)
+    finally:
+        c.close()
+
+
+def py_uvarint_len(x):
+    return len(py_uvarint(x))
