@@ -238,16 +238,35 @@ class Bench:
         torch.cuda.current_stream(self.dev).wait_stream(sm)
 
     def verify(self):
-        """Size-independent checks on the last chunk of the last step: every
-        status is OK, every decoded payload digest equals its source digest,
-        and the decoded rows equal the input rows."""
+        """Every record of the batch, after the timed steps: each chunk is
+        encoded and decoded once more (untimed, one stream) and checked by
+        size-independent properties: every encode and decode status is OK,
+        every decoded payload's length and position-aware digest equal its
+        source's, and the decoded rows equal the generator's input rows."""
         torch.cuda.synchronize()
-        a, b, sl = self.last
-        L, c, s = self.lib, sl.codec.ctx, torch.cuda.current_stream(self.dev).cuda_stream
+        sl = self.slots[0]
+        L, c = self.lib, sl.codec.ctx
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        ok = True
+        for a, b in self.chunks:
+            n = b - a
+            self._sizes(sl.codec, a, b, sl.out_off, sl.status, s)
+            _lib.check(L.honu_encode(c, P(self.meta) + 352 * a, P(self.var), self.var_len, P(self.acl),
+                                     self.acl_len, P(self.reg), self.reg_len, P(self.payload),
+                                     P(self.off) + 8 * a, n, P(sl.out), self.out_cap, P(sl.out_off),
+                                     P(sl.status), s), "encode")
+            _lib.check(L.honu_decode_batch(c, P(sl.out), P(sl.out_off), n, P(sl.dmeta), P(sl.dinfo),
+                                           P(sl.dacl), self.acl_cap, P(sl.dreg), self.reg_cap,
+                                           P(sl.data), self.data_cap, P(sl.totals), s), "decode")
+            ok &= self._verify_chunk(a, b, sl, s)
+        return bool(ok)
+
+    def _verify_chunk(self, a, b, sl, s):
+        L, c = self.lib, sl.codec.ctx
         n = b - a
         st = sl.status[: 4 * n].view(torch.int32)
         info = sl.dinfo[: 32 * n].view(torch.int64).view(n, 4)
-        ms = info[:, 2].contiguous().view(torch.int32)
+        ms = info[:, 2].contiguous().view(torch.int32)  # data_status, meta_status pairs
         dsrc = torch.empty(8 * n, dtype=torch.uint8, device=self.dev)
         ddst = torch.empty(8 * n, dtype=torch.uint8, device=self.dev)
         _lib.check(L.honu_digest_records(c, P(self.payload), P(self.off) + 8 * a, 0, n, P(dsrc), s),
@@ -520,6 +539,8 @@ def main():
             "zero_copy_decode_chunk_records": zc["records"],
         },
         "verified": ok_all,
+        "verified_scope": None if ok_all is None else
+        "every record of every rank: statuses, payload lengths + digests, decoded rows vs input rows",
     }
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
