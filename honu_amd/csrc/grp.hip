@@ -30,6 +30,12 @@ namespace honu {
 #define GO_MAX_ALLOC (1ull << 48)  // runtime maxAlloc, linux/amd64
 
 constexpr int GRP = 16;                       // lanes per record
+#ifndef FILL_G
+#define FILL_G 16                             // decode fill: lanes per record
+#endif
+#ifndef FILL_K
+#define FILL_K 2                              // decode fill: ACL entries per lane in flight
+#endif
 constexpr uint32_t GCAP = 2048;               // stage window, bytes
 constexpr uint32_t GPAD = 16;                 // front pad of the encode stage
 constexpr uint32_t GSTAGE = GPAD + GCAP + 32; // + slack for 32-byte windows
@@ -832,7 +838,7 @@ HONU_DEV void k_decode_fill_grp_one(uint64_t i, const uint8_t *__restrict__ rec,
             const uint64_t end = sc.rec_end;
             const uint64_t ap = sc.acl_pos & GRP_POS_MASK;
             if (na && (sc.acl_pos & GRP_ACL_FAST)) {
-                constexpr int K = 4;  // entries per lane loaded before any store
+                constexpr int K = FILL_K;  // entries per lane loaded before any store
                 for (uint64_t j0 = r; j0 < na; j0 += (uint64_t)G * K) {
                     uint64_t lo[K], hi[K];
                     uint32_t pm[K];
@@ -1068,7 +1074,9 @@ hipError_t launch_decode_fill_grp(const uint8_t *rec, uint64_t n, honu_meta *met
                                   uint32_t *reg, uint64_t reg_cap, uint8_t *data,
                                   uint64_t data_cap, int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_decode_fill_grp<GRP>, grp_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, rec, n, meta,
+    const uint64_t b = (n * FILL_G + HONU_BLOCK - 1) / HONU_BLOCK;
+    const dim3 grid((unsigned)(max_blocks > 0 && b > (uint64_t)max_blocks ? (uint64_t)max_blocks : b));
+    hipLaunchKernelGGL(k_decode_fill_grp<FILL_G>, grid, dim3(HONU_BLOCK), 0, s, rec, n, meta,
                        info, scratch, reg_inline, counts, offs, acl, acl_cap, reg, reg_cap, data,
                        data_cap);
     return hipGetLastError();

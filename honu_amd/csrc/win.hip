@@ -62,9 +62,13 @@ struct LaneWin {
         if (want != NOWIN) wb = want;
     }
     HONU_DEV bool has16(uint64_t p) const { return wb != NOWIN && p >= wb && p - wb <= WB - 16; }
+    // The LDS and the global read stay two instructions of their own address
+    // spaces: a select between the two pointers compiles to flat_load_ubyte
+    // (counted by both vmcnt and lgkmcnt, LDS hits at flat latency).
     HONU_DEV uint32_t u8(uint64_t p) const {
-        if (wb != NOWIN && p >= wb && p - wb < WB) return mine()[p - wb];
-        return rec[p];
+        if (wb != NOWIN && p >= wb && p - wb < WB)
+            return ((const __attribute__((address_space(3))) uint8_t *)mine())[p - wb];
+        return ((const __attribute__((address_space(1))) uint8_t *)rec)[p];
     }
     HONU_DEV void fetch16(uint64_t p, uint64_t end, uint64_t &lo, uint64_t &hi) const {
         if (has16(p)) {
