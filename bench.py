@@ -49,8 +49,10 @@ def parse_args():
     p.add_argument("--shape", default="large")
     p.add_argument("--chunk-gib", type=float, default=12.0,
                    help="encoded bytes per device-resident chunk (output slots are sized by it)")
-    p.add_argument("--min-chunks", type=int, default=4,
-                   help="at least this many chunks, so metadata and copies can overlap")
+    p.add_argument("--min-chunks", type=int, default=-1,
+                   help="at least this many chunks, so metadata and copies can overlap "
+                        "(-1 = auto: 1 for batches under 8 GiB, where the launch tails of "
+                        "extra chunks cost more than the overlap gains, else 4)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-seconds", type=float, default=20.0,
                    help="total CPU-baseline time, split between the 1-thread and all-core legs")
@@ -102,12 +104,12 @@ class Bench:
         # chunk boundaries by bytes (payload + ~1.1 KB of header/metadata per record)
         est = np.diff(off.astype(np.int64)) + 1100
         cum = np.concatenate([[0], np.cumsum(est)])
-        budget = min(args.chunk_gib * 2**30, cum[-1] / max(1, args.min_chunks) + 1)
-        bounds = [0]
-        while bounds[-1] < N:
-            a = bounds[-1]
-            b = int(np.searchsorted(cum, cum[a] + budget, side="right")) - 1
-            bounds.append(min(N, max(b, a + 1)))
+        # equal-byte chunks: enough that each fits --chunk-gib, at least --min-chunks
+        min_chunks = args.min_chunks if args.min_chunks >= 0 else (1 if cum[-1] < 8 * 2**30 else 4)
+        k = max(1, min_chunks, int(np.ceil(cum[-1] / (args.chunk_gib * 2**30))))
+        k = min(k, N)
+        cuts = np.searchsorted(cum, cum[-1] * np.arange(1, k) / k, side="left")
+        bounds = sorted(set([0, N] + [int(c) for c in cuts if 0 < c < N]))
         self.chunks = list(zip(bounds[:-1], bounds[1:]))
         C = max(b - a for a, b in self.chunks)
         self.C = C
@@ -266,7 +268,9 @@ class Bench:
         n = b - a
         st = sl.status[: 4 * n].view(torch.int32)
         info = sl.dinfo[: 32 * n].view(torch.int64).view(n, 4)
-        ms = info[:, 2].contiguous().view(torch.int32)  # data_status, meta_status pairs
+        # data_status, meta_status pairs ((n, 1) int64 -> (n, 2) int32; the
+        # reshape keeps the last stride 1 even for a one-record chunk)
+        ms = info[:, 2].reshape(n, 1).contiguous().view(torch.int32)
         dsrc = torch.empty(8 * n, dtype=torch.uint8, device=self.dev)
         ddst = torch.empty(8 * n, dtype=torch.uint8, device=self.dev)
         _lib.check(L.honu_digest_records(c, P(self.payload), P(self.off) + 8 * a, 0, n, P(dsrc), s),
