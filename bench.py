@@ -183,13 +183,18 @@ class Bench:
                                        n, P(out_off), P(status), s), "sizes")
         _lib.check(L.honu_exclusive_scan(c, P(out_off), n, P(out_off), s), "scan")
 
-    def step(self, timed=False):
+    def step(self, timed=False, check=None):
         """Chunk k: metadata work (sizes, scan, headers+tails, parse, tables) on
         stream sm, payload copies on stream sc; two slots so chunk k+1's metadata
-        work overlaps chunk k's copies. Only bytes outside the payloads are
-        touched by the metadata kernels, so they may run beside the copies."""
+        work overlaps chunk k's copies. The encode copy needs only the output
+        offsets and statuses (sizes + scan): it writes the payload bytes, the
+        metadata kernels write only the bytes around them (byte-exact stores at
+        the shared 16-byte chunks), so it runs beside the header/tail encoder.
+        check(a, b, slot) -> bool, when given, runs after each chunk completes
+        (verification pass); the result is the AND of its answers."""
         L = self.lib
         sm, sc = self.sm, self.sc
+        ok = True
         for k, (a, b) in enumerate(self.chunks):
             n = b - a
             sl = self.slots[k % len(self.slots)]
@@ -198,12 +203,12 @@ class Bench:
                 sm.wait_event(sl.free)
             ms = sm.cuda_stream
             self._sizes(sl.codec, a, b, sl.out_off, sl.status, ms)
+            ev_off = torch.cuda.Event()
+            ev_off.record(sm)
             _lib.check(L.honu_encode_records(c, P(self.meta) + 352 * a, P(self.var), P(self.acl),
                                              P(self.reg), P(self.off) + 8 * a, n, P(sl.out),
                                              self.out_cap, P(sl.out_off), P(sl.status), ms),
                        "encode_records")
-            ev_meta = torch.cuda.Event()
-            ev_meta.record(sm)
             _lib.check(L.honu_decode_parse(c, P(sl.out), P(sl.out_off), n, P(sl.dmeta),
                                            P(sl.dinfo), ms), "decode_parse")
             _lib.check(L.honu_decode_tables(c, P(sl.out), n, P(sl.dmeta), P(sl.dinfo),
@@ -213,7 +218,7 @@ class Bench:
             ev_fill = torch.cuda.Event()
             ev_fill.record(sm)
             cs = sc.cuda_stream
-            sc.wait_event(ev_meta)
+            sc.wait_event(ev_off)
             e0 = torch.cuda.Event(enable_timing=True) if timed else None
             e1 = torch.cuda.Event(enable_timing=True) if timed else None
             if timed:
@@ -236,32 +241,23 @@ class Bench:
             sl.free = torch.cuda.Event()
             sl.free.record(sc)
             self.last = (a, b, sl)
+            if check is not None:
+                torch.cuda.synchronize()
+                ok &= check(a, b, sl)
         torch.cuda.current_stream(self.dev).wait_stream(sc)
         torch.cuda.current_stream(self.dev).wait_stream(sm)
+        return ok
 
     def verify(self):
-        """Every record of the batch, after the timed steps: each chunk is
-        encoded and decoded once more (untimed, one stream) and checked by
-        size-independent properties: every encode and decode status is OK,
-        every decoded payload's length and position-aware digest equal its
-        source's, and the decoded rows equal the generator's input rows."""
+        """Every record of the batch, after the timed steps: one more pipelined
+        step (same streams, slots and overlap as the timed ones) whose chunks
+        are each checked when complete by size-independent properties: every
+        encode and decode status is OK, every decoded payload's length and
+        position-aware digest equal its source's, and the decoded rows equal
+        the generator's input rows."""
         torch.cuda.synchronize()
-        sl = self.slots[0]
-        L, c = self.lib, sl.codec.ctx
         s = torch.cuda.current_stream(self.dev).cuda_stream
-        ok = True
-        for a, b in self.chunks:
-            n = b - a
-            self._sizes(sl.codec, a, b, sl.out_off, sl.status, s)
-            _lib.check(L.honu_encode(c, P(self.meta) + 352 * a, P(self.var), self.var_len, P(self.acl),
-                                     self.acl_len, P(self.reg), self.reg_len, P(self.payload),
-                                     P(self.off) + 8 * a, n, P(sl.out), self.out_cap, P(sl.out_off),
-                                     P(sl.status), s), "encode")
-            _lib.check(L.honu_decode_batch(c, P(sl.out), P(sl.out_off), n, P(sl.dmeta), P(sl.dinfo),
-                                           P(sl.dacl), self.acl_cap, P(sl.dreg), self.reg_cap,
-                                           P(sl.data), self.data_cap, P(sl.totals), s), "decode")
-            ok &= self._verify_chunk(a, b, sl, s)
-        return bool(ok)
+        return bool(self.step(check=lambda a, b, sl: self._verify_chunk(a, b, sl, s)))
 
     def _verify_chunk(self, a, b, sl, s):
         L, c = self.lib, sl.codec.ctx
