@@ -46,6 +46,9 @@ _PROTOS = {
     "honu_decode_batch": (I32, [P, P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),
     "honu_decode_keys": (I32, [P, P, P, U64, P, P, P]),
     "honu_decode_headers": (I32, [P, P, P, U64, P, P]),
+    "honu_decode_data": (I32, [P, P, P, U64, P, P, U64, P, P]),
+    "honu_decode_data_place": (I32, [P, P, P, U64, P, U64, P, P]),
+    "honu_decode_data_copy": (I32, [P, P, U64, P, P, P]),
     "honu_system_sizes": (I32, [P, P, U64, P, U64, P, U64, P, U64, U64, P, P, P]),
     "honu_system_encode": (I32, [P, P, P, P, P, P, U64, P, U64, P, P, P]),
     "honu_system_marshal_batch": (I32, [P, P, P, U64, P, U64, P, U64, P, U64, U64, P, U64, P, P,

@@ -377,6 +377,49 @@ int32_t honu_decode_headers(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t 
     return HONU_OK;
 }
 
+int32_t honu_decode_data_place(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                               uint64_t n, honu_record_info *d_info, uint64_t data_cap,
+                               uint64_t *d_totals, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n > ctx->max_n) return HONU_E_WORKSPACE;
+    if (n && (!d_rec || !d_rec_off || !d_info)) return arg_fail("null pointer");
+    if (!aligned(d_info, 8)) return arg_fail("record info must be 8-byte aligned");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        if (d_totals) HIPCHK(hipMemsetAsync(d_totals, 0, 8, s));
+        return HONU_OK;
+    }
+    // spans -> exclusive scan of the aligned sizes (offs[n] = total) -> place
+    HIPCHK(launch_decode_spans(d_rec, d_rec_off, n, d_info, ctx->scratch, ctx->counts, s));
+    HIPCHK(launch_scan(ctx->counts, n, 1, ctx->offs, ctx->offs + n, ctx->partials, s));
+    HIPCHK(launch_decode_data_place(n, d_info, ctx->offs, data_cap, s));
+    if (d_totals)
+        HIPCHK(hipMemcpyAsync(d_totals, ctx->offs + n, 8, hipMemcpyDeviceToDevice, s));
+    return HONU_OK;
+}
+
+int32_t honu_decode_data_copy(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n,
+                              const honu_record_info *d_info, uint8_t *d_data, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n > ctx->max_n) return HONU_E_WORKSPACE;
+    if (n && (!d_rec || !d_info || !d_data)) return arg_fail("null pointer");
+    if (!aligned(d_data, 16)) return arg_fail("data arena must be 16-byte aligned");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_span_copy(ctx->geom, d_rec, n, d_info, ctx->scratch, ctx->offs, d_data,
+                            (hipStream_t)stream));
+    return HONU_OK;
+}
+
+int32_t honu_decode_data(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                         uint64_t n, honu_record_info *d_info, uint8_t *d_data, uint64_t data_cap,
+                         uint64_t *d_totals, void *stream) {
+    if (n && !d_data) return arg_fail("data arena");
+    int32_t st = honu_decode_data_place(ctx, d_rec, d_rec_off, n, d_info, data_cap, d_totals, stream);
+    if (st) return st;
+    return honu_decode_data_copy(ctx, d_rec, n, d_info, d_data, stream);
+}
+
 int32_t honu_decode_keys(honu_ctx *ctx, const honu_meta *d_meta, const honu_record_info *d_info,
                          uint64_t n, uint8_t *d_keys, int32_t *d_key_status, void *stream) {
     if (!ctx) return arg_fail("ctx");

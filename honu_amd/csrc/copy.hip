@@ -65,6 +65,27 @@ struct DecodeSegments {
     }
 };
 
+// Segment i of honu_decode_data: logical start = offs[i] (one column, the
+// destination offset), src = rec + scratch[i].data_src.
+struct SpanSegments {
+    const uint8_t *rec;
+    const honu_record_info *info;
+    const DecodeScratch *scratch;
+    const uint64_t *offs;
+    uint8_t *data;
+
+    HONU_DEV uint64_t start(uint64_t i) const { return offs[i]; }
+    HONU_DEV uint64_t lo() const { return 0; }
+    HONU_DEV uint64_t end(uint64_t i, uint64_t total_abs) const { (void)total_abs; return offs[i + 1]; }
+    HONU_DEV bool get(uint64_t i, uint64_t &len, const uint8_t *&src, uint8_t *&dst) const {
+        if (info[i].data_status != HONU_OK) return false;
+        len = info[i].data_len;
+        src = rec + scratch[i].data_src;
+        dst = data + offs[i];
+        return len != 0;
+    }
+};
+
 #define SMALL_SEG_WAVES_FACTOR 4
 
 template <class Seg, int UNROLL, bool NT>
@@ -196,6 +217,14 @@ hipError_t launch_encode_copy(const LaunchGeom &g, const uint8_t *payload,
     if (n == 0) return hipSuccess;
     EncodeSegments seg{payload, payload_off, out, out_off, status};
     return launch_copy(g, seg, n, payload_off + n, s);
+}
+
+hipError_t launch_span_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t n,
+                            const honu_record_info *info, const DecodeScratch *scratch,
+                            const uint64_t *offs, uint8_t *data, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    SpanSegments seg{rec, info, scratch, offs, data};
+    return launch_copy(g, seg, n, offs + n, s);
 }
 
 hipError_t launch_decode_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t n,

@@ -156,6 +156,14 @@ hipError_t launch_system_fill(const uint8_t *rec, uint64_t n, honu_collection *r
 
 hipError_t launch_decode_headers(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                  honu_record_info *info, hipStream_t s);
+hipError_t launch_decode_spans(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                               honu_record_info *info, DecodeScratch *scratch, uint64_t *counts,
+                               hipStream_t s);
+hipError_t launch_decode_data_place(uint64_t n, honu_record_info *info, const uint64_t *offs,
+                                    uint64_t data_cap, hipStream_t s);
+hipError_t launch_span_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t n,
+                            const honu_record_info *info, const DecodeScratch *scratch,
+                            const uint64_t *offs, uint8_t *data, hipStream_t s);
 
 // Exclusive scan of K interleaved u64 columns: out[i*K+c] = sum_{j<i} in[j*K+c];
 // totals[c] = full sum. `partials` needs scan_partials_len(n, K) u64.

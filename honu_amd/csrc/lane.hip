@@ -611,9 +611,14 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
 // ------------------------------------------------------------------------
 // headers only: StorageVersion, Data, Tombstone (object.go:47-52,85-134)
 // ------------------------------------------------------------------------
+// SPANS: also hand the payload's absolute offset (scratch.data_src) and its
+// 16-byte aligned size (counts[i], one column) to honu_decode_data's scan and
+// copy.
+template <bool SPANS>
 __global__ __launch_bounds__(HONU_BLOCK) void k_decode_headers(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
-    honu_record_info *__restrict__ info) {
+    honu_record_info *__restrict__ info, DecodeScratch *__restrict__ scratch,
+    uint64_t *__restrict__ counts) {
     for (uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * HONU_BLOCK) {
         const uint64_t beg = rec_off[i], end = rec_off[i + 1];
@@ -652,16 +657,61 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_headers(
         inf.tombstone = (v1 && d == 0) ? 1 : 0;
 #pragma unroll
         for (int k = 0; k < 6; k++) inf._pad[k] = 0;
+        if constexpr (SPANS) {
+            scratch[i].data_src = inf.data_off;
+            counts[i] = (inf.data_len + 15) & ~15ull;
+        }
         store_info(info + i, inf);
     }
+}
+
+// honu_decode_data, after the scan: data_off relative to the data arena, or
+// HONU_ERR_CAPACITY for a payload that does not fit (then nothing is copied).
+__global__ __launch_bounds__(HONU_BLOCK) void k_decode_data_place(
+    uint64_t n, honu_record_info *__restrict__ info, const uint64_t *__restrict__ offs,
+    uint64_t data_cap) {
+    for (uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * HONU_BLOCK) {
+        honu_record_info *p = info + i;
+        if (p->data_status != HONU_OK || !p->data_len) continue;
+        const uint64_t o = offs[i];
+        if (o > data_cap || p->data_len > data_cap - o) {
+            p->data_status = HONU_ERR_CAPACITY;
+            p->data_off = 0;
+            p->data_len = 0;
+        } else {
+            p->data_off = o;
+        }
+    }
+}
+
+static dim3 flat_grid(uint64_t n) {
+    const uint64_t b = (n + HONU_BLOCK - 1) / HONU_BLOCK;
+    return dim3((unsigned)(b > 65536 ? 65536 : b));
 }
 
 hipError_t launch_decode_headers(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                  honu_record_info *info, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const uint64_t b = (n + HONU_BLOCK - 1) / HONU_BLOCK;
-    hipLaunchKernelGGL(k_decode_headers, dim3((unsigned)(b > 65536 ? 65536 : b)), dim3(HONU_BLOCK),
-                       0, s, rec, rec_off, n, info);
+    hipLaunchKernelGGL(k_decode_headers<false>, flat_grid(n), dim3(HONU_BLOCK), 0, s, rec, rec_off,
+                       n, info, nullptr, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_spans(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                               honu_record_info *info, DecodeScratch *scratch, uint64_t *counts,
+                               hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_decode_headers<true>, flat_grid(n), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
+                       info, scratch, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_data_place(uint64_t n, honu_record_info *info, const uint64_t *offs,
+                                    uint64_t data_cap, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_decode_data_place, flat_grid(n), dim3(HONU_BLOCK), 0, s, n, info, offs,
+                       data_cap);
     return hipGetLastError();
 }
 

@@ -311,6 +311,26 @@ int32_t honu_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
 int32_t honu_decode_headers(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
                             uint64_t n, honu_record_info *d_info, void *stream);
 
+/* Object.Data() (object.go:85-99) of every record materialised into a packed
+ * data arena, without Metadata(): Data() needs only the header, so this runs
+ * beside (on another stream and context) or without a Metadata() parse. d_info
+ * is written as by honu_decode_headers, except that data_off is relative to
+ * d_data: payloads are 16-byte aligned and back to back in record order, the
+ * offsets honu_decode_fill assigns. A payload that does not fit data_cap gets
+ * HONU_ERR_CAPACITY in data_status and is not copied. d_totals (optional,
+ * device, 1 x u64) receives the data-arena bytes the batch needs. */
+int32_t honu_decode_data(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                         uint64_t n, honu_record_info *d_info, uint8_t *d_data, uint64_t data_cap,
+                         uint64_t *d_totals, void *stream);
+/* honu_decode_data in two phases, to schedule or time the copy apart: place
+ * (header walk, offsets, capacity; d_info complete after it) and the payload
+ * copy (same ctx and d_info, after place on the same stream). */
+int32_t honu_decode_data_place(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                               uint64_t n, honu_record_info *d_info, uint64_t data_cap,
+                               uint64_t *d_totals, void *stream);
+int32_t honu_decode_data_copy(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n,
+                              const honu_record_info *d_info, uint8_t *d_data, void *stream);
+
 /* Object.Key() (object.go:57-64 -> keys.New, keys/keys.go:42-51) for every
  * decoded record: 0x01 | ObjectID | BE64(VID) | BE32(PID), 29 bytes per
  * record at d_keys + 29*i. d_key_status[i] = meta_status, or HONU_ERR_PANIC

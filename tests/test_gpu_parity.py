@@ -404,3 +404,61 @@ def test_payload_length_varint_boundaries(oracle_lib):
 
 def py_uvarint_len(x):
     return len(py_uvarint(x))
+
+
+def test_decode_data_without_metadata(oracle_lib):
+    """honu_decode_data: Object.Data() materialised without Metadata(): the
+    record info's data fields, StorageVersion and Tombstone equal the oracle's
+    full decode (meta_status is HONU_UNPARSED), data offsets equal the ones
+    the materialising decode assigns, payload bytes are bit-exact — on a batch
+    with corrupted and truncated records; then a data arena too small for the
+    batch gives HONU_ERR_CAPACITY exactly for the payloads past it."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    hb = gen_host_batch(17, "mixed", 0, 700)
+    rec, off, _ = oracle_lib.marshal_batch(hb)
+    objs = [rec[int(off[i]):int(off[i + 1])].tobytes() for i in range(700)]
+    rng = np.random.default_rng(17)
+    for i in range(0, 700, 23):
+        b = bytearray(objs[i])
+        b[int(rng.integers(0, min(len(b), 6)))] ^= 0xFF  # header bytes: version / length
+        objs[i] = bytes(b[: int(rng.integers(0, len(b) + 1))])
+    objs += [b"", b"\x01", b"\x01\x00", b"\x01\x00\x00", b"\x02\x00\x00"]
+    n = len(objs)
+    roff = np.zeros(n + 1, np.uint64)
+    roff[1:] = np.cumsum([len(o) for o in objs])
+    arena = np.frombuffer(b"".join(objs), np.uint8)
+    _, oinfo, _, _, odata, otot = oracle_lib.decode_batch(arena, roff, True)
+    c = hobj.Codec(0, n)
+    try:
+        L = hobj._lib
+        d_rec, d_off = dev(arena, c), dev(roff, c)
+        cap = int(otot[2]) + 64
+        d_info, d_data, d_tot = c._empty(32 * n), c._empty(cap), c._empty(8)
+        L.check(c.lib.honu_decode_data(c.ctx, L.ptr(d_rec), L.ptr(d_off), n, L.ptr(d_info),
+                                       L.ptr(d_data), cap, L.ptr(d_tot), c.stream), "decode_data")
+        torch.cuda.synchronize()
+        info = hobj._to_host(d_info, 32 * n, np.uint8).view(oinfo.dtype)
+        data = hobj._to_host(d_data, cap, np.uint8)
+        assert int(hobj._to_host(d_tot, 8, np.uint64)[0]) == int(otot[2])
+        for f in ("data_off", "data_len", "data_status", "storage_version", "tombstone"):
+            assert np.array_equal(info[f], oinfo[f]), f
+        assert (info["meta_status"] == 11).all()
+        assert len(set(oinfo["data_status"].tolist())) >= 3
+        for i in range(n):
+            if oinfo[i]["data_status"] == 0 and oinfo[i]["data_len"]:
+                o, ln = int(oinfo[i]["data_off"]), int(oinfo[i]["data_len"])
+                assert data[o:o + ln].tobytes() == odata[o:o + ln].tobytes(), i
+        # a smaller arena: exactly the payloads ending past it fail with CAPACITY
+        small = int(otot[2]) // 2
+        L.check(c.lib.honu_decode_data(c.ctx, L.ptr(d_rec), L.ptr(d_off), n, L.ptr(d_info),
+                                       L.ptr(d_data), small, 0, c.stream), "decode_data")
+        torch.cuda.synchronize()
+        info2 = hobj._to_host(d_info, 32 * n, np.uint8).view(oinfo.dtype)
+        ok = oinfo["data_status"] == 0
+        past = ok & (oinfo["data_off"] + oinfo["data_len"] > small) & (oinfo["data_len"] > 0)
+        assert (info2["data_status"][past] == 9).all() and past.any()
+        keep = ok & ~past
+        assert np.array_equal(info2["data_off"][keep], oinfo["data_off"][keep])
+    finally:
+        c.close()
