@@ -67,6 +67,9 @@ def parse_args():
                         "beside them (0 = no cap; -1 = auto: 2 when records average > 64 KiB, "
                         "where the copies dominate, else no cap)")
     p.add_argument("--copy-prio", type=int, default=1, help="copy stream gets high priority")
+    p.add_argument("--encode-copy-after", choices=["scan", "meta"], default="scan",
+                   help="start a chunk's encode payload copy after its sizes + scan, or after "
+                        "its header/tail encoder too")
     p.add_argument("--copy-blocks", type=int, default=0,
                    help="workgroups per CU of the payload copy engine (0 = library default)")
     return p.parse_args()
@@ -209,6 +212,9 @@ class Bench:
                                              P(self.reg), P(self.off) + 8 * a, n, P(sl.out),
                                              self.out_cap, P(sl.out_off), P(sl.status), ms),
                        "encode_records")
+            if self.args.encode_copy_after == "meta":
+                ev_off = torch.cuda.Event()
+                ev_off.record(sm)
             _lib.check(L.honu_decode_parse(c, P(sl.out), P(sl.out_off), n, P(sl.dmeta),
                                            P(sl.dinfo), ms), "decode_parse")
             _lib.check(L.honu_decode_tables(c, P(sl.out), n, P(sl.dmeta), P(sl.dinfo),
