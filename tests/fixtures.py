@@ -21,6 +21,7 @@ import base64
 import datetime as _dt
 import json
 import os
+import numpy as np
 
 from honu_amd.metadata import (AccessControl, Compression, Encryption, Metadata, Publisher, Scalar,
                                SchemaVersion, Version)
@@ -298,3 +299,39 @@ def py_marshal_system(c) -> bytes:
             o += b"\x00" if f is None else b"\x01" + _frame(f.Name) + bytes([f.Type]) + f.Collection
     o += py_varint(c.Created) + py_varint(c.Modified) + b"\x00"
     return bytes(o)
+
+
+def extreme_metas(n=96, seed=29):
+    """Every varint at its widest and narrowest: PID/region/schema numbers at
+    0 and 2^32-1 (5 bytes), VIDs at 2^64-1 (10 bytes), times and compression
+    levels at INT64_MIN / INT64_MAX / -1 / 1 (zig-zag 10 bytes and 1 byte),
+    frame lengths at 0, 127, 128 and 16384, region ids at every varint width,
+    permission and flag bytes at 0 and 255."""
+    from honu_amd.metadata import (AccessControl, Compression, Encryption, Metadata, Publisher,
+                                   Scalar, SchemaVersion, Version)
+    rng = np.random.default_rng(seed)
+    U32, U64, I64 = [0, 1, 127, 128, 2**32 - 1], [0, 2**63, 2**64 - 1], [-2**63, 2**63 - 1, -1, 1, 0]
+    LENS = [0, 1, 127, 128, 16384]
+    pick = lambda xs, i: xs[i % len(xs)]  # noqa: E731
+    metas, datas = [], []
+    for i in range(n):
+        ln = pick(LENS, i // 3)
+        metas.append(Metadata(
+            ObjectID=rng.bytes(16), CollectionID=rng.bytes(16),
+            Version=Version(Scalar(pick(U32, i), pick(U64, i)), pick(U32, i + 1),
+                            Scalar(pick(U32, i + 2), pick(U64, i + 1)) if i % 2 else None,
+                            bool(i % 3 == 0), pick(I64, i)),
+            Schema=SchemaVersion("s" * pick(LENS, i), pick(U32, i), pick(U32, i + 3), pick(U32, i + 4))
+            if i % 4 else None,
+            MIME="m" * ln, Owner=rng.bytes(16), Group=rng.bytes(16), Permissions=255 * (i % 2),
+            ACL=[AccessControl(rng.bytes(16), 255 * (j % 2)) for j in range(i % 5)] or None,
+            WriteRegions=[pick(U32, i + j) for j in range(i % 4)] if i % 6 else None,
+            Publisher=Publisher(rng.bytes(16), rng.bytes(16), rng.bytes(pick(LENS, i + 1)) or None,
+                                "u" * pick(LENS, i + 2)) if i % 3 else None,
+            Encryption=Encryption("k" * pick(LENS, i + 3), rng.bytes(pick(LENS, i + 4)) or None,
+                                  rng.bytes(pick(LENS, i)) or None, rng.bytes(pick(LENS, i + 1)) or None,
+                                  i % 6, (i + 1) % 6, (i + 2) % 6) if i % 5 else None,
+            Compression=Compression(i % 5, pick(I64, i + 1)) if i % 7 else None,
+            Flags=255 * ((i + 1) % 2), Created=pick(I64, i + 2), Modified=pick(I64, i + 3)))
+        datas.append(rng.bytes(pick(LENS, i)) if i % 9 else None)
+    return metas, datas

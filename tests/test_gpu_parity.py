@@ -462,3 +462,19 @@ def test_decode_data_without_metadata(oracle_lib):
         assert np.array_equal(info2["data_off"][keep], oinfo["data_off"][keep])
     finally:
         c.close()
+
+
+def test_extreme_values_parity(codec, oracle_lib):
+    from fixtures import extreme_metas
+    metas, datas = extreme_metas()
+    hb = pack_batch(metas, datas)
+    out, off, st = gpu_marshal(codec, hb)
+    oout, ooff, ost = oracle_lib.marshal_batch(hb)
+    assert np.array_equal(st, ost) and (st == 0).all()
+    assert np.array_equal(off, ooff)
+    assert out.tobytes() == oout.tobytes()
+    for materialize in (False, True):
+        meta, info, acl, reg, data = assert_decode_equal(oracle_lib, codec, oout, ooff, materialize)
+        assert (info["meta_status"] == 0).all()
+    for i in range(len(metas)):
+        assert unpack_row(meta[i], oout, acl, reg) == normalize(metas[i]), i

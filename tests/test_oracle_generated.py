@@ -56,3 +56,21 @@ def test_digest_host_properties():
     b = bytearray(a)
     b[100], b[101] = b[101], b[100]
     assert digest_host(a) != digest_host(bytes(b))
+
+
+def test_extreme_values_roundtrip(oracle_lib):
+    """Widest and narrowest varints, zero-length and 16 KiB frames, nil and
+    present sub-structs (tests/fixtures.py:extreme_metas): the oracle's bytes
+    equal the independent Python encoder's, and decode restores every field."""
+    from fixtures import extreme_metas
+    from honu_amd.metadata import pack_batch
+    metas, datas = extreme_metas()
+    hb = pack_batch(metas, datas)
+    out, off, st = oracle_lib.marshal_batch(hb)
+    assert (st == 0).all()
+    for i, (m, d) in enumerate(zip(metas, datas)):
+        assert bytes(out[int(off[i]):int(off[i + 1])]) == py_marshal(m, d), i
+    meta, info, acl, reg, data, tot = oracle_lib.decode_batch(out, off, materialize=True)
+    assert (info["meta_status"] == 0).all()
+    for i, m in enumerate(metas):
+        assert unpack_row(meta[i], out, acl, reg) == normalize(m), i
