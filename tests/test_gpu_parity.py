@@ -28,7 +28,7 @@ def codec(request):
     16 lanes, per lane, and lane encode/parse with the group size pass/fill."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    c = hobj.Codec(0, 1 << 16)
+    c = hobj.Codec(0, 1 << 18)
     hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", request.param), "param")
     yield c
     c.close()
@@ -478,3 +478,16 @@ def test_extreme_values_parity(codec, oracle_lib):
         assert (info["meta_status"] == 0).all()
     for i in range(len(metas)):
         assert unpack_row(meta[i], oout, acl, reg) == normalize(metas[i]), i
+
+
+def test_decode_parse_full_waves(codec, oracle_lib):
+    """A batch of 2^17 + 77 records (many grid-stride rounds of the window
+    parse and group fill, a partial last wave): bit-exact rows, info and tables."""
+    n = (1 << 17) + 77
+    hb = gen_host_batch(23, "small", 0, n)
+    rec, off, _ = oracle_lib.marshal_batch(hb)
+    meta, info, acl, reg, data, tot = gpu_decode(codec, rec, off)
+    ometa, oinfo, oacl, oreg, odata, otot = oracle_lib.decode_batch(rec, off, False)
+    assert np.array_equal(tot, otot) and info.tobytes() == oinfo.tobytes()
+    assert meta.tobytes() == ometa.tobytes()
+    assert acl.tobytes() == oacl.tobytes() and reg.tobytes() == oreg.tobytes()
