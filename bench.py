@@ -65,7 +65,7 @@ def parse_args():
     p.add_argument("--lane-blocks", type=int, default=-1,
                    help="workgroups per CU for the lane/group metadata kernels while copies run "
                         "beside them (0 = no cap; -1 = auto: 2 when records average > 64 KiB, "
-                        "where the copies dominate, else no cap)")
+                        "where the copies dominate, 4 above 8 KiB, else no cap)")
     p.add_argument("--copy-prio", type=int, default=1, help="copy stream gets high priority")
     p.add_argument("--encode-copy-after", choices=["scan", "meta"], default="scan",
                    help="start a chunk's encode payload copy after its sizes + scan, or after "
@@ -156,8 +156,9 @@ class Bench:
                       for _ in range(nslots)]
         ncu = torch.cuda.get_device_properties(self.dev).multi_processor_count
         lane_blocks = args.lane_blocks
-        if lane_blocks < 0:
-            lane_blocks = 2 if self.total_rec_bytes / N > 65536 else 0
+        if lane_blocks < 0:  # measured: tools/overlap_sweep.sh, tools/ab_env.sh
+            avg = self.total_rec_bytes / N
+            lane_blocks = 2 if avg > 65536 else (4 if avg > 8192 else 0)
         self.lane_blocks = 0 if args.serial else lane_blocks
         for sl in self.slots:
             if args.copy_blocks:
