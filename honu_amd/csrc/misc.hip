@@ -59,15 +59,29 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_digest(const uint8_t *__restrict
         const uint64_t sh = (uint64_t)p & 7u;
         const uint64_t *a = reinterpret_cast<const uint64_t *>(p - sh);
         uint64_t acc = 0;
-        for (uint64_t k = lane_id(); k < nw; k += HONU_WAVE) {
-            uint64_t w = a[k];
-            if (sh) {
-                w >>= 8 * sh;
-                if (8 * k + (8 - sh) < len) w |= a[k + 1] << (64 - 8 * sh);
+        constexpr int U = 4;  // words per lane with their loads in flight together
+        for (uint64_t k0 = lane_id(); k0 < nw; k0 += U * HONU_WAVE) {
+            uint64_t lo[U], hi[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint64_t k = k0 + (uint64_t)u * HONU_WAVE;
+                lo[u] = hi[u] = 0;
+                if (k < nw) {
+                    lo[u] = a[k];
+                    if (sh && 8 * k + (8 - sh) < len) hi[u] = a[k + 1];
+                }
             }
-            const uint64_t valid = len - 8 * k;
-            if (valid < 8) w &= (1ull << (8 * valid)) - 1;
-            acc += digest_term(w, k);
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint64_t k = k0 + (uint64_t)u * HONU_WAVE;
+                if (k < nw) {
+                    uint64_t w = lo[u];
+                    if (sh) w = (w >> (8 * sh)) | (hi[u] << (64 - 8 * sh));
+                    const uint64_t valid = len - 8 * k;
+                    if (valid < 8) w &= (1ull << (8 * valid)) - 1;
+                    acc += digest_term(w, k);
+                }
+            }
         }
         acc = wave_sum(acc);
         if (lane_id() == 0) digest[i] = acc + splitmix64(len);
