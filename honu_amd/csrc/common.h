@@ -164,7 +164,9 @@ HONU_DEV void wave_copy_bytes(uint8_t *__restrict__ dst, const uint8_t *__restri
 // never touched. Source chunks are read with aligned 16-byte loads: an
 // aligned 16-byte block holding at least one source byte never crosses a
 // page, so the over-read is always mapped.
-template <int UNROLL = 4, bool NT = false>
+// NT: non-temporal cache policy, 0 none, 1 loads and stores, 2 loads only,
+// 3 stores only
+template <int UNROLL = 4, int NT = 0>
 HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint64_t n) {
     if (n == 0) return;
     const uint32_t lane = lane_id();
@@ -188,10 +190,10 @@ HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ s
             u32x4 v[UNROLL];
 #pragma unroll
             for (int u = 0; u < UNROLL; u++)
-                if (c + u * HONU_WAVE < chunks) v[u] = ld16<NT>(&s4[c + u * HONU_WAVE]);
+                if (c + u * HONU_WAVE < chunks) v[u] = ld16<(NT == 1 || NT == 2)>(&s4[c + u * HONU_WAVE]);
 #pragma unroll
             for (int u = 0; u < UNROLL; u++)
-                if (c + u * HONU_WAVE < chunks) st16<NT>(&d4[c + u * HONU_WAVE], v[u]);
+                if (c + u * HONU_WAVE < chunks) st16<(NT == 1 || NT == 3)>(&d4[c + u * HONU_WAVE], v[u]);
         }
     } else {
         const u32x4 *__restrict__ s4 = reinterpret_cast<const u32x4 *>(src - p);
@@ -200,14 +202,14 @@ HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ s
 #pragma unroll
             for (int u = 0; u < UNROLL; u++) {
                 if (c + u * HONU_WAVE < chunks) {
-                    lo[u] = ld16<NT>(&s4[c + u * HONU_WAVE]);
-                    hi[u] = ld16<NT>(&s4[c + u * HONU_WAVE + 1]);
+                    lo[u] = ld16<(NT == 1 || NT == 2)>(&s4[c + u * HONU_WAVE]);
+                    hi[u] = ld16<(NT == 1 || NT == 2)>(&s4[c + u * HONU_WAVE + 1]);
                 }
             }
 #pragma unroll
             for (int u = 0; u < UNROLL; u++)
                 if (c + u * HONU_WAVE < chunks)
-                    st16<NT>(&d4[c + u * HONU_WAVE], funnel16(lo[u], hi[u], p));
+                    st16<(NT == 1 || NT == 3)>(&d4[c + u * HONU_WAVE], funnel16(lo[u], hi[u], p));
         }
     }
     if (tail) {

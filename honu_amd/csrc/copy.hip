@@ -88,7 +88,7 @@ struct SpanSegments {
 
 #define SMALL_SEG_WAVES_FACTOR 4
 
-template <class Seg, int UNROLL, bool NT>
+template <class Seg, int UNROLL, int NT>
 __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t n,
                                                                const uint64_t *__restrict__ total_p) {
     uint64_t W = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
@@ -178,13 +178,13 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_sweep(Seg seg, uint64_t n,
             const uint64_t x = s > lo ? s : lo;
             const uint64_t e = s + len;
             const uint64_t y = e < hi ? e : hi;
-            if (x < y) wave_copy<UNROLL, false>(dst + (x - s), src + (x - s), y - x);
+            if (x < y) wave_copy<UNROLL, 0>(dst + (x - s), src + (x - s), y - x);
         }
     }
 }
 
 // Copy-engine variants: 0-5 contiguous per-wave ranges {unroll, non-temporal};
-// 6-7 the sweep form. Variant 0 is the default; the others exist for the
+// 6-7 the sweep form; 11 / 12 non-temporal loads only / stores only. Variant 0 is the default; the others exist for the
 // measurement sweeps in tools/tune_copy.py.
 template <class Seg>
 static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
@@ -201,12 +201,14 @@ static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
         return hipGetLastError();
     }
     switch (g.copy_variant) {
-    case 1: hipLaunchKernelGGL((k_copy_segments<Seg, 8, false>), grid, block, 0, s, seg, n, total); break;
-    case 2: hipLaunchKernelGGL((k_copy_segments<Seg, 4, true>), grid, block, 0, s, seg, n, total); break;
-    case 3: hipLaunchKernelGGL((k_copy_segments<Seg, 8, true>), grid, block, 0, s, seg, n, total); break;
-    case 4: hipLaunchKernelGGL((k_copy_segments<Seg, 2, false>), grid, block, 0, s, seg, n, total); break;
-    case 5: hipLaunchKernelGGL((k_copy_segments<Seg, 16, false>), grid, block, 0, s, seg, n, total); break;
-    default: hipLaunchKernelGGL((k_copy_segments<Seg, 4, false>), grid, block, 0, s, seg, n, total); break;
+    case 1: hipLaunchKernelGGL((k_copy_segments<Seg, 8, 0>), grid, block, 0, s, seg, n, total); break;
+    case 2: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 1>), grid, block, 0, s, seg, n, total); break;
+    case 3: hipLaunchKernelGGL((k_copy_segments<Seg, 8, 1>), grid, block, 0, s, seg, n, total); break;
+    case 4: hipLaunchKernelGGL((k_copy_segments<Seg, 2, 0>), grid, block, 0, s, seg, n, total); break;
+    case 5: hipLaunchKernelGGL((k_copy_segments<Seg, 16, 0>), grid, block, 0, s, seg, n, total); break;
+    case 11: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 2>), grid, block, 0, s, seg, n, total); break;
+    case 12: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 3>), grid, block, 0, s, seg, n, total); break;
+    default: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0>), grid, block, 0, s, seg, n, total); break;
     }
     return hipGetLastError();
 }
