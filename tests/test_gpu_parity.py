@@ -491,3 +491,65 @@ def test_decode_parse_full_waves(codec, oracle_lib):
     assert np.array_equal(tot, otot) and info.tobytes() == oinfo.tobytes()
     assert meta.tobytes() == ometa.tobytes()
     assert acl.tobytes() == oacl.tobytes() and reg.tobytes() == oreg.tobytes()
+
+
+def test_hip_graph_capture_replay(oracle_lib):
+    """The ABI's calls neither allocate nor synchronise (include/honu_codec.h),
+    so a whole marshal + decode + keys sequence is captured into one hipGraph
+    (torch.cuda.CUDAGraph over the capturing stream) and replayed: outputs are
+    recomputed from the device inputs at every replay, bit-exact."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    L = hobj._lib
+    n = 1500
+    hb = gen_host_batch(37, "mixed", 0, n)
+    oout, ooff, _ = oracle_lib.marshal_batch(hb)
+    ometa, oinfo, oacl, oreg, odata, otot = oracle_lib.decode_batch(oout, ooff, True)
+    c = hobj.Codec(0, n)
+    try:
+        db = hobj.DeviceBatch.from_host(hb, c.torch_device)
+        total = int(ooff[-1])
+        out_off, status, out = c._empty(8 * (n + 1)), c._empty(4 * n), c._empty(total)
+        meta, info, totals = c._empty(352 * n), c._empty(32 * n), c._empty(32)
+        acl_cap, reg_cap, data_cap = total, total, total + 16 * n
+        acl, reg, data = c._empty(20 * acl_cap), c._empty(4 * reg_cap), c._empty(data_cap)
+        keys, kst = c._empty(29 * n), c._empty(4 * n)
+
+        def seq():
+            c.encode_sizes(db, out_off, status)
+            c.scan(out_off, n, out_off)
+            c.encode(db, out, total, out_off, status)
+            L.check(c.lib.honu_decode_batch(c.ctx, L.ptr(out), L.ptr(out_off), n, L.ptr(meta),
+                                            L.ptr(info), L.ptr(acl), acl_cap, L.ptr(reg), reg_cap,
+                                            L.ptr(data), data_cap, L.ptr(totals), c.stream), "decode")
+            L.check(c.lib.honu_decode_keys(c.ctx, L.ptr(meta), L.ptr(info), n, L.ptr(keys),
+                                           L.ptr(kst), c.stream), "keys")
+
+        seq()  # warm up outside the capture (module loading)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            seq()
+        for t in (out, meta, info, acl, reg, data, keys, totals):
+            t.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert hobj._to_host(out, total, np.uint8).tobytes() == oout.tobytes()
+        assert hobj._to_host(meta, 352 * n, np.uint8).tobytes() == ometa.tobytes()
+        assert hobj._to_host(info, 32 * n, np.uint8).tobytes() == oinfo.tobytes()
+        assert np.array_equal(hobj._to_host(totals, 24, np.uint64), otot)
+        na, nr, nd = (int(x) for x in otot)
+        assert hobj._to_host(acl, 20 * na, np.uint8).tobytes() == oacl.tobytes()
+        assert hobj._to_host(reg, 4 * nr, np.uint8).tobytes() == oreg.tobytes()
+        assert hobj._to_host(data, nd, np.uint8).tobytes() == odata[:nd].tobytes()
+        # the replay reads the inputs again: a changed payload byte shows up
+        p = int(hb.payload_off[7])
+        db.payload[p:p + 1].bitwise_xor_(torch.tensor([0xFF], dtype=torch.uint8,
+                                                      device=c.torch_device))
+        g.replay()
+        torch.cuda.synchronize()
+        got = hobj._to_host(out, total, np.uint8)
+        diff = np.nonzero(got != oout)[0]
+        assert len(diff) == 1 and got[diff[0]] == oout[diff[0]] ^ 0xFF
+    finally:
+        c.close()
