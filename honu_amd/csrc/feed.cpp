@@ -15,6 +15,9 @@
 #include <cstring>
 
 #include "../../include/honu_codec.h"
+#include "host_copy.h"
+
+using honu::host_copy;
 
 namespace {
 
@@ -201,13 +204,24 @@ int32_t honu_feed_append_batch(honu_feed *f, const uint8_t *arena, const uint64_
                                uint64_t *appended) {
     if (!f || (n && (!arena || !off)) || !appended) return HONU_E_ARG;
     *appended = 0;
-    for (uint64_t i = 0; i < n; i++) {
-        if (off[i + 1] < off[i]) return HONU_E_ARG;
-        const int32_t st = honu_feed_append(f, arena + off[i], off[i + 1] - off[i]);
-        if (st != HONU_OK) return st;
-        *appended = i + 1;
+    int32_t err = HONU_OK;
+    Slot *sp = filling(f, &err);
+    if (!sp) return err;
+    Slot &s = *sp;
+    // the run of records that fits: they are contiguous in the arena, so they
+    // land as one (multi-threaded) copy
+    uint64_t k = 0;
+    for (; k < n && s.n + k < f->cap_n; k++) {
+        if (off[k + 1] < off[k]) return HONU_E_ARG;
+        if (off[k + 1] - off[0] > f->cap_bytes - s.bytes) break;
     }
-    return HONU_OK;
+    const uint64_t bytes = k ? off[k] - off[0] : 0;
+    if (bytes) host_copy({honu::HostCopy{s.h_rec + s.bytes, arena + off[0], bytes}}, bytes);
+    for (uint64_t j = 0; j < k; j++) s.h_off[s.n + j + 1] = s.bytes + (off[j + 1] - off[0]);
+    s.n += k;
+    s.bytes += bytes;
+    *appended = k;
+    return k == n ? HONU_OK : HONU_ERR_CAPACITY;
 }
 
 uint64_t honu_feed_pending(const honu_feed *f) {

@@ -9,13 +9,16 @@
 //
 // Two slots, as the read feed (feed.cpp). The encoded records come back by a
 // D2H copy sized by an upper bound of the batch's encoded bytes that append()
-// keeps (put_bound below), so submit() never has to wait for the size pass.
+// keeps (kFixedBound below), so submit() never has to wait for the size pass.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
 #include <cstring>
+#include <thread>
+#include <vector>
 
 #include "../../include/honu_codec.h"
+#include "host_copy.h"
 
 namespace {
 
@@ -196,6 +199,95 @@ static void live_spans(const honu_meta &r, honu_span *out[8], bool live[8], honu
     live[4] = live[5] = live[6] = live[7] = p & HONU_HAS_ENCRYPTION;
 }
 
+// A record's placement: what append() checks and counts before any byte
+// moves (phase 1), then where its bytes go in the slot (phase 2).
+struct PutPlan {
+    honu_meta w;  // the row, absent sub-structs' spans zeroed
+    uint64_t span_bytes = 0, nacl = 0, nreg = 0, need = 0, bound = 0;
+    uint64_t var_at = 0, acl_at = 0, reg_at = 0, pay_at = 0;  // slot positions
+};
+
+// Phase 1: validate the row's spans and lists against the caller's arrays
+// and size the record (HONU_ERR_INPUT: nothing may be appended).
+static int32_t put_plan(const honu_put_feed *f, const honu_meta *row, const uint8_t *var,
+                        uint64_t var_len, const honu_acl *acl, uint64_t acl_len,
+                        const uint32_t *regions, uint64_t regions_len, uint64_t data_len,
+                        PutPlan &p) {
+    p.w = *row;
+    honu_span *spans[8];
+    bool live[8];
+    live_spans(*row, spans, live, p.w);
+    p.span_bytes = p.nacl = p.nreg = 0;
+    if (row->present & HONU_HAS_META) {
+        for (int k = 0; k < 8; k++) {
+            if (!live[k]) {
+                *spans[k] = honu_span{0, 0};
+                continue;
+            }
+            const honu_span sv = *spans[k];
+            if (sv.len && (!var || sv.off > var_len || sv.len > var_len - sv.off)) return HONU_ERR_INPUT;
+            p.span_bytes += sv.len;
+        }
+        p.nacl = row->acl_count;
+        p.nreg = row->regions_count;
+        if (p.nacl && (!acl || row->acl_off > acl_len || p.nacl > acl_len - row->acl_off))
+            return HONU_ERR_INPUT;
+        if (p.nreg && (!regions || row->regions_off > regions_len || p.nreg > regions_len - row->regions_off))
+            return HONU_ERR_INPUT;
+    } else {  // Marshal(nil, data): the encoder reports HONU_ERR_PANIC
+        for (int k = 0; k < 8; k++) *spans[k] = honu_span{0, 0};
+        p.w.acl_count = p.w.regions_count = 0;
+    }
+    if (p.nacl > f->cap_bytes / sizeof(honu_acl) || p.nreg > f->cap_bytes / 4) return HONU_ERR_CAPACITY;
+    p.need = p.span_bytes + data_len + sizeof(honu_acl) * p.nacl + 4 * p.nreg;
+    p.bound = kFixedBound + p.span_bytes + data_len + 18 * p.nacl + 5 * p.nreg;
+    return HONU_OK;
+}
+
+// Phase 2: copy the referenced bytes to the plan's slot positions, compacted,
+// and store the rebased row as record `idx` of the slot.
+static void put_fill(Slot &s, uint64_t idx, const PutPlan &p, const honu_meta *row,
+                     const uint8_t *var, const honu_acl *acl, const uint32_t *regions,
+                     const uint8_t *data, uint64_t data_len) {
+    honu_meta w = p.w;
+    honu_span *spans[8];
+    bool live[8];
+    live_spans(w, spans, live, w);
+    uint64_t at = p.var_at;
+    for (int k = 0; k < 8; k++) {
+        honu_span &sv = *spans[k];
+        if (!sv.len) {
+            sv.off = 0;
+            continue;
+        }
+        std::memcpy(s.h_var + at, var + sv.off, sv.len);
+        sv.off = at;
+        at += sv.len;
+    }
+    if (p.nacl) std::memcpy(s.h_acl + p.acl_at, acl + row->acl_off, sizeof(honu_acl) * p.nacl);
+    if (p.nreg) std::memcpy(s.h_reg + p.reg_at, regions + row->regions_off, 4 * p.nreg);
+    w.acl_off = p.nacl ? p.acl_at : 0;
+    w.regions_off = p.nreg ? p.reg_at : 0;
+    if (data_len) std::memcpy(s.h_pay + p.pay_at, data, data_len);
+    s.h_meta[idx] = w;
+    s.h_poff[idx + 1] = p.pay_at + data_len;
+}
+
+// Reserve the plan's positions at the slot's fill point.
+static void put_place(Slot &s, PutPlan &p, uint64_t data_len) {
+    p.var_at = s.var;
+    p.acl_at = s.acl;
+    p.reg_at = s.reg;
+    p.pay_at = s.pay;
+    s.var += p.span_bytes;
+    s.acl += p.nacl;
+    s.reg += p.nreg;
+    s.pay += data_len;
+    s.budget += p.need;
+    s.bound += p.bound;
+    s.n += 1;
+}
+
 int32_t honu_put_feed_append(honu_put_feed *f, const honu_meta *row, const uint8_t *var,
                              uint64_t var_len, const honu_acl *acl, uint64_t acl_len,
                              const uint32_t *regions, uint64_t regions_len, const uint8_t *data,
@@ -205,57 +297,13 @@ int32_t honu_put_feed_append(honu_put_feed *f, const honu_meta *row, const uint8
     Slot *sp = put_filling(f, &err);
     if (!sp) return err;
     Slot &s = *sp;
-    honu_meta w = *row;
-    uint64_t span_bytes = 0, nacl = 0, nreg = 0;
-    honu_span *spans[8];
-    bool live[8];
-    live_spans(*row, spans, live, w);
-    if (row->present & HONU_HAS_META) {
-        for (int k = 0; k < 8; k++) {
-            if (!live[k]) {
-                *spans[k] = honu_span{0, 0};
-                continue;
-            }
-            const honu_span sv = *spans[k];
-            if (sv.len && (!var || sv.off > var_len || sv.len > var_len - sv.off)) return HONU_ERR_INPUT;
-            span_bytes += sv.len;
-        }
-        nacl = row->acl_count;
-        nreg = row->regions_count;
-        if (nacl && (!acl || row->acl_off > acl_len || nacl > acl_len - row->acl_off)) return HONU_ERR_INPUT;
-        if (nreg && (!regions || row->regions_off > regions_len || nreg > regions_len - row->regions_off))
-            return HONU_ERR_INPUT;
-    } else {  // Marshal(nil, data): the encoder reports HONU_ERR_PANIC
-        for (int k = 0; k < 8; k++) *spans[k] = honu_span{0, 0};
-        w.acl_count = w.regions_count = 0;
-    }
-    if (nacl > f->cap_bytes / sizeof(honu_acl) || nreg > f->cap_bytes / 4) return HONU_ERR_CAPACITY;
-    const uint64_t need = span_bytes + data_len + sizeof(honu_acl) * nacl + 4 * nreg;
-    if (s.n == f->cap_n || need > f->cap_bytes - s.budget) return HONU_ERR_CAPACITY;
-    // copy the referenced bytes, compacted, and rebase the row onto them
-    for (int k = 0; k < 8; k++) {
-        honu_span &sv = *spans[k];
-        if (!sv.len) {
-            sv.off = 0;
-            continue;
-        }
-        std::memcpy(s.h_var + s.var, var + sv.off, sv.len);
-        sv.off = s.var;
-        s.var += sv.len;
-    }
-    if (nacl) std::memcpy(s.h_acl + s.acl, acl + row->acl_off, sizeof(honu_acl) * nacl);
-    if (nreg) std::memcpy(s.h_reg + s.reg, regions + row->regions_off, 4 * nreg);
-    w.acl_off = nacl ? s.acl : 0;
-    w.regions_off = nreg ? s.reg : 0;
-    s.acl += nacl;
-    s.reg += nreg;
-    if (data_len) std::memcpy(s.h_pay + s.pay, data, data_len);
-    s.pay += data_len;
-    s.h_meta[s.n] = w;
-    s.n += 1;
-    s.h_poff[s.n] = s.pay;
-    s.budget += need;
-    s.bound += kFixedBound + span_bytes + data_len + 18 * nacl + 5 * nreg;
+    PutPlan p;
+    err = put_plan(f, row, var, var_len, acl, acl_len, regions, regions_len, data_len, p);
+    if (err) return err;
+    if (s.n == f->cap_n || p.need > f->cap_bytes - s.budget) return HONU_ERR_CAPACITY;
+    const uint64_t idx = s.n;
+    put_place(s, p, data_len);
+    put_fill(s, idx, p, row, var, acl, regions, data, data_len);
     return HONU_OK;
 }
 
@@ -266,15 +314,62 @@ int32_t honu_put_feed_append_batch(honu_put_feed *f, const honu_meta *rows, uint
                                    uint64_t *appended) {
     if (!f || (n && (!rows || !payload_off)) || !appended) return HONU_E_ARG;
     *appended = 0;
+    int32_t st = HONU_OK;
+    Slot *sp = put_filling(f, &st);
+    if (!sp) return st;
+    Slot &s = *sp;
+    // phase 1, serial: check and place every record that goes in
+    std::vector<PutPlan> plans;
+    plans.reserve(n < f->cap_n - s.n ? n : f->cap_n - s.n);
+    const uint64_t first = s.n;
+    uint64_t bytes = 0;
     for (uint64_t i = 0; i < n; i++) {
         const uint64_t a = payload_off[i], b = payload_off[i + 1];
-        if (b < a) return HONU_ERR_INPUT;
-        const int32_t st = honu_put_feed_append(f, rows + i, var, var_len, acl, acl_len, regions,
-                                                regions_len, payload ? payload + a : nullptr, b - a);
-        if (st != HONU_OK) return st;
-        *appended = i + 1;
+        if (b < a || (b > a && !payload)) {
+            st = b < a ? HONU_ERR_INPUT : HONU_E_ARG;
+            break;
+        }
+        PutPlan p;
+        st = put_plan(f, rows + i, var, var_len, acl, acl_len, regions, regions_len, b - a, p);
+        if (st) break;
+        if (s.n == f->cap_n || p.need > f->cap_bytes - s.budget) {
+            st = HONU_ERR_CAPACITY;
+            break;
+        }
+        put_place(s, p, b - a);
+        plans.push_back(p);
+        bytes += p.need;
     }
-    return HONU_OK;
+    // phase 2: the copies, record ranges over a few threads for big batches
+    const uint64_t k = plans.size();
+    auto fill = [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t i = lo; i < hi; i++) {
+            const uint64_t a = payload_off[i], b = payload_off[i + 1];
+            put_fill(s, first + i, plans[i], rows + i, var, acl, regions,
+                     payload ? payload + a : nullptr, b - a);
+        }
+    };
+    const unsigned T = bytes >= honu::kParallelCopyMin && k > 1 ? honu::host_copy_threads() : 1;
+    if (T == 1) {
+        fill(0, k);
+    } else {  // equal-byte record ranges
+        std::vector<uint64_t> cuts{0};
+        uint64_t acc = 0, t = 1;
+        for (uint64_t i = 0; i < k && t < T; i++) {
+            acc += plans[i].need;
+            if (acc >= bytes * t / T) {
+                cuts.push_back(i + 1);
+                t++;
+            }
+        }
+        cuts.push_back(k);
+        std::vector<std::thread> pool;
+        for (size_t c = 1; c + 1 < cuts.size(); c++) pool.emplace_back(fill, cuts[c], cuts[c + 1]);
+        fill(cuts[0], cuts[1]);
+        for (std::thread &th : pool) th.join();
+    }
+    *appended = k;
+    return st;
 }
 
 uint64_t honu_put_feed_pending(const honu_put_feed *f) {
