@@ -553,3 +553,37 @@ def test_hip_graph_capture_replay(oracle_lib):
         assert len(diff) == 1 and got[diff[0]] == oout[diff[0]] ^ 0xFF
     finally:
         c.close()
+
+
+def test_decode_fuzz_mutations(codec, oracle_lib):
+    """20,000 mutants of valid records (byte flips, varint-byte rewrites to
+    0x80/0xff/0x00/0x01, insertions, deletions and truncations inside the
+    Metadata tail), decoded bit-exact against the oracle: rows, record info
+    (every status), ACL/region tables and materialised payloads."""
+    rng = np.random.default_rng(2024)
+    hb = gen_host_batch(55, "small", 0, 400)
+    rec, off, _ = oracle_lib.marshal_batch(hb)
+    valid = [rec[int(off[i]):int(off[i + 1])].tobytes() for i in range(400)]
+    objs = []
+    for k in range(20000):
+        v = bytearray(valid[k % 400])
+        hdr = 1 + len(py_uvarint(int(hb.payload_off[k % 400 + 1] - hb.payload_off[k % 400])))
+        tail0 = hdr + int(hb.payload_off[k % 400 + 1] - hb.payload_off[k % 400])
+        kind = k % 5
+        pos = int(rng.integers(tail0, len(v)))
+        if kind == 0:
+            v[pos] ^= int(rng.integers(1, 256))
+        elif kind == 1:
+            v[pos] = int(rng.choice([0x80, 0xFF, 0x00, 0x01]))
+        elif kind == 2:
+            v[pos:pos] = rng.integers(0, 256, int(rng.integers(1, 4)), dtype=np.uint8).tobytes()
+        elif kind == 3:
+            del v[pos:pos + int(rng.integers(1, 4))]
+        else:
+            v = v[:pos]
+        objs.append(bytes(v))
+    o = np.zeros(len(objs) + 1, np.uint64)
+    o[1:] = np.cumsum([len(x) for x in objs])
+    arena = np.frombuffer(b"".join(objs), np.uint8)
+    meta, info, acl, reg, data = assert_decode_equal(oracle_lib, codec, arena, o, materialize=True)
+    assert len(set(info["meta_status"].tolist())) >= 5
