@@ -587,3 +587,53 @@ def test_decode_fuzz_mutations(codec, oracle_lib):
     arena = np.frombuffer(b"".join(objs), np.uint8)
     meta, info, acl, reg, data = assert_decode_equal(oracle_lib, codec, arena, o, materialize=True)
     assert len(set(info["meta_status"].tolist())) >= 5
+
+
+def _random_metas(n, seed):
+    from honu_amd.metadata import (AccessControl, Compression, Encryption, Metadata, Publisher,
+                                   Scalar, SchemaVersion, Version)
+    rng = np.random.default_rng(seed)
+    ri = lambda bits: int(rng.integers(0, 2**bits, dtype=np.uint64)) if bits < 64 else \
+        int(rng.integers(0, 2**63)) * 2 + int(rng.integers(0, 2))  # noqa: E731
+    rs = lambda: int(rng.integers(-2**62, 2**62)) * int(rng.choice([1, 2]))  # noqa: E731
+    ln = lambda: int(rng.choice([0, 1, 5, 127, 128, 129, int(rng.integers(0, 400))]))  # noqa: E731
+    p = lambda q: rng.random() < q  # noqa: E731
+    metas, datas = [], []
+    for _ in range(n):
+        w = lambda: int(rng.choice([7, 14, 21, 28, 32]))  # noqa: E731
+        metas.append(Metadata(
+            ObjectID=rng.bytes(16), CollectionID=rng.bytes(16),
+            Version=Version(Scalar(ri(w()), ri(int(rng.choice([7, 35, 63, 64])))), ri(w()),
+                            Scalar(ri(w()), ri(40)) if p(.5) else None, p(.5), rs()) if p(.8) else None,
+            Schema=SchemaVersion("x" * ln(), ri(w()), ri(w()), ri(w())) if p(.7) else None,
+            MIME="m" * ln(), Owner=rng.bytes(16), Group=rng.bytes(16),
+            Permissions=int(rng.integers(0, 256)),
+            ACL=[AccessControl(rng.bytes(16), int(rng.integers(0, 256))) if p(.9) else None
+                 for _ in range(int(rng.integers(0, 40)))] or None,
+            WriteRegions=[ri(w()) for _ in range(int(rng.integers(0, 13)))] if p(.8) else None,
+            Publisher=Publisher(rng.bytes(16), rng.bytes(16), rng.bytes(ln()) or None, "u" * ln())
+            if p(.7) else None,
+            Encryption=Encryption("k" * ln(), rng.bytes(ln()) or None, rng.bytes(ln()) or None,
+                                  rng.bytes(ln()) or None, int(rng.integers(0, 256)),
+                                  int(rng.integers(0, 256)), int(rng.integers(0, 256))) if p(.7) else None,
+            Compression=Compression(int(rng.integers(0, 256)), rs()) if p(.7) else None,
+            Flags=int(rng.integers(0, 256)), Created=rs() if p(.9) else 0, Modified=rs() if p(.9) else 0))
+        datas.append(rng.bytes(int(rng.integers(0, 3000))) if p(.9) else None)
+    return metas, datas
+
+
+def test_encode_fuzz_random_metadata(codec, oracle_lib):
+    """3,000 random Metadata (every sub-struct present or nil, frames of 0-400
+    bytes around the 1/2-byte length boundary, nil ACL entries, region and
+    integer values of every varint width, negative times): encoded bytes
+    bit-exact vs the oracle, and decoded back to the same fields."""
+    metas, datas = _random_metas(3000, 77)
+    hb = pack_batch(metas, datas)
+    out, off, st = gpu_marshal(codec, hb)
+    oout, ooff, ost = oracle_lib.marshal_batch(hb)
+    assert np.array_equal(st, ost) and (st == 0).all()
+    assert np.array_equal(off, ooff) and out.tobytes() == oout.tobytes()
+    meta, info, acl, reg, data = assert_decode_equal(oracle_lib, codec, oout, ooff, materialize=True)
+    assert (info["meta_status"] == 0).all()
+    for i in range(0, 3000, 7):
+        assert unpack_row(meta[i], oout, acl, reg) == normalize(metas[i]), i
