@@ -177,6 +177,7 @@ class Bench:
                    if nslots == 2 else self.sm)
         self.events = None
         self.last = None
+        self.nchunk = 0  # chunks issued so far, across steps: slots alternate globally
         torch.cuda.synchronize()
 
     def _sizes(self, codec, a, b, out_off, status, s):
@@ -201,7 +202,10 @@ class Bench:
         ok = True
         for k, (a, b) in enumerate(self.chunks):
             n = b - a
-            sl = self.slots[k % len(self.slots)]
+            # the slot after the previous chunk's, also across steps, so a
+            # step's first chunk overlaps the previous step's last one
+            sl = self.slots[self.nchunk % len(self.slots)]
+            self.nchunk += 1
             c = sl.codec.ctx
             if sl.free is not None:
                 sm.wait_event(sl.free)
