@@ -1,3 +1,6 @@
+#!/bin/bash
+# Interleaved A/B of the working-tree bench.py against the committed one:
+#   git show HEAD:bench.py > bench_head.py && tools/ab_bench_head.sh (on the GPU box)
 set -u
 : > gpurun_out/ab_x.txt
 for r in 1 2; do
