@@ -82,12 +82,15 @@ def P(t):
 class Slot:
     """Output buffers + codec context of one in-flight chunk."""
 
-    def __init__(self, dev, chunk, out_cap, acl_cap, reg_cap, data_cap):
+    def __init__(self, dev, chunk, out_cap, acl_cap, reg_cap, data_cap, pad=(0, 0)):
         E = lambda nb: torch.empty(int(nb), dtype=torch.uint8, device=dev)  # noqa: E731
         self.codec = Codec(dev.index, max_records=chunk)
         self.out_off, self.status = E(8 * (chunk + 1)), E(4 * chunk + 16)
-        self.out, self.dmeta, self.dinfo = E(out_cap), E(352 * chunk), E(32 * chunk)
-        self.dacl, self.dreg, self.data = E(20 * acl_cap), E(4 * reg_cap), E(data_cap)
+        # pad: byte offsets of the records and data arenas inside their
+        # allocations (multiples of 256), for placement experiments
+        self.out = E(out_cap + pad[0])[pad[0]:]
+        self.dmeta, self.dinfo = E(352 * chunk), E(32 * chunk)
+        self.dacl, self.dreg, self.data = E(20 * acl_cap), E(4 * reg_cap), E(data_cap + pad[1])[pad[1]:]
         self.totals = E(32)
         self.free = None  # event: the slot's last copy finished
 
