@@ -1,3 +1,4 @@
+#!/bin/bash
 set -u
 # TLB counters of the copy kernels under three separate bench processes
 # (tests whether the between-process spread is address translation).
