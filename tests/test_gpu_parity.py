@@ -637,3 +637,41 @@ def test_encode_fuzz_random_metadata(codec, oracle_lib):
     assert (info["meta_status"] == 0).all()
     for i in range(0, 3000, 7):
         assert unpack_row(meta[i], oout, acl, reg) == normalize(metas[i]), i
+
+
+def test_concurrent_contexts_on_streams(oracle_lib):
+    """Two contexts on two streams, their batches in flight together (the ABI:
+    calls on distinct streams are concurrent, one context per stream): both
+    encodes and decodes bit-exact."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    L = hobj._lib
+    runs = []
+    for seed, shape in ((61, "small"), (62, "mixed")):
+        n = 1200
+        hb = gen_host_batch(seed, shape, 0, n)
+        oout, ooff, _ = oracle_lib.marshal_batch(hb)
+        c = hobj.Codec(0, n)
+        db = hobj.DeviceBatch.from_host(hb, c.torch_device)
+        total = int(ooff[-1])
+        bufs = dict(out_off=c._empty(8 * (n + 1)), status=c._empty(4 * n), out=c._empty(total),
+                    meta=c._empty(352 * n), info=c._empty(32 * n), acl=c._empty(20 * total),
+                    reg=c._empty(4 * total), totals=c._empty(32))
+        runs.append((c, db, n, total, bufs, oout, ooff, torch.cuda.Stream()))
+    torch.cuda.synchronize()
+    for c, db, n, total, b, _, _, s in runs:  # issue both before waiting for either
+        with torch.cuda.stream(s):
+            c.encode_sizes(db, b["out_off"], b["status"])
+            c.scan(b["out_off"], n, b["out_off"])
+            c.encode(db, b["out"], total, b["out_off"], b["status"])
+            L.check(c.lib.honu_decode_batch(c.ctx, L.ptr(b["out"]), L.ptr(b["out_off"]), n,
+                                            L.ptr(b["meta"]), L.ptr(b["info"]), L.ptr(b["acl"]),
+                                            total, L.ptr(b["reg"]), total, 0, 0, L.ptr(b["totals"]),
+                                            c.stream), "decode")
+    torch.cuda.synchronize()
+    for c, db, n, total, b, oout, ooff, _ in runs:
+        assert hobj._to_host(b["out"], total, np.uint8).tobytes() == oout.tobytes()
+        ometa, oinfo, *_ = oracle_lib.decode_batch(oout, ooff, False)
+        assert hobj._to_host(b["meta"], 352 * n, np.uint8).tobytes() == ometa.tobytes()
+        assert hobj._to_host(b["info"], 32 * n, np.uint8).tobytes() == oinfo.tobytes()
+        c.close()
