@@ -1,0 +1,143 @@
+/*
+ * c_abi_demo.c — the batch flow a cgo shim runs (INTEGRATION.md MarshalBatch /
+ * DecodeBatch), written against include/honu_codec.h in plain C: no Python, no
+ * torch, only the library's own pinned/device allocation helpers, plain
+ * pointers, sizes and the null stream. Built by honu_amd/Makefile; run by
+ * tests/test_c_abi.py on a GPU box.
+ *
+ *   c_abi_demo [shape] [n]   shape: 0 Small, 1 Medium, 2 Large, 4 Mixed
+ *
+ * Steps: generate a synthetic host batch (rows, var arena, ACL and region
+ * tables, payloads) -> H2D -> honu_marshal_batch -> D2H of offsets/records ->
+ * honu_decode_batch (zero copy) -> D2H of rows/info -> honu_decode_batch
+ * materialising -> D2H of payloads; checks every status, the decoded rows'
+ * scalar fields against the input rows and every payload's digest. Exit 0 and
+ * one "ok" line on success.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/honu_codec.h"
+
+#define CHECK(x)                                                                          \
+    do {                                                                                  \
+        int32_t st_ = (x);                                                                \
+        if (st_ != HONU_OK) {                                                             \
+            fprintf(stderr, "%s:%d %s -> %d (%s: %s)\n", __FILE__, __LINE__, #x, st_,     \
+                    honu_status_string(st_), honu_last_error());                          \
+            return 1;                                                                     \
+        }                                                                                 \
+    } while (0)
+#define NEED(p)                                                          \
+    do {                                                                 \
+        if (!(p)) {                                                      \
+            fprintf(stderr, "%s:%d allocation failed: %s\n", __FILE__, __LINE__, #p); \
+            return 1;                                                    \
+        }                                                                \
+    } while (0)
+
+static void *h2d(const void *h, uint64_t bytes) {
+    void *d = honu_device_alloc(bytes + 16);
+    if (d && bytes && honu_memcpy_h2d(d, h, bytes, NULL) != HONU_OK) return NULL;
+    return d;
+}
+
+int main(int argc, char **argv) {
+    const int32_t shape = argc > 1 ? atoi(argv[1]) : HONU_SHAPE_SMALL;
+    const uint64_t n = argc > 2 ? strtoull(argv[2], NULL, 10) : 4096;
+    const uint64_t seed = 12345;
+    int32_t err = 0;
+    honu_ctx *ctx = honu_ctx_create(0, n, &err);
+    if (!ctx) {
+        fprintf(stderr, "honu_ctx_create: %s (%s)\n", honu_status_string(err), honu_last_error());
+        return 2;
+    }
+    /* 1. the host batch, as the Go side's flatten() would build it */
+    uint64_t tot[4];
+    honu_gen_totals(seed, shape, 0, n, tot); /* var bytes, ACL entries, regions, payload bytes */
+    honu_meta *rows = (honu_meta *)honu_host_alloc(sizeof(honu_meta) * n);
+    uint8_t *var = (uint8_t *)honu_host_alloc(tot[0] + 16);
+    honu_acl *acl = (honu_acl *)honu_host_alloc(sizeof(honu_acl) * tot[1] + 16);
+    uint32_t *reg = (uint32_t *)honu_host_alloc(4 * tot[2] + 16);
+    uint64_t *poff = (uint64_t *)honu_host_alloc(8 * (n + 1));
+    uint8_t *pay = (uint8_t *)honu_host_alloc(tot[3] + 16);
+    NEED(rows && var && acl && reg && poff && pay);
+    honu_gen_meta(seed, shape, 0, n, rows, var, acl, reg, poff);
+    honu_gen_payload_host(seed, 0, n, poff, pay);
+    /* 2. H2D */
+    void *d_rows = h2d(rows, sizeof(honu_meta) * n), *d_var = h2d(var, tot[0]);
+    void *d_acl = h2d(acl, sizeof(honu_acl) * tot[1]), *d_reg = h2d(reg, 4 * tot[2]);
+    void *d_poff = h2d(poff, 8 * (n + 1)), *d_pay = h2d(pay, tot[3]);
+    NEED(d_rows && d_var && d_acl && d_reg && d_poff && d_pay);
+    /* 3. Marshal: an upper bound for the output arena (payload + 4 KiB/record) */
+    const uint64_t cap = tot[3] + 4096 * n;
+    uint64_t *d_off = (uint64_t *)honu_device_alloc(8 * (n + 1));
+    int32_t *d_st = (int32_t *)honu_device_alloc(4 * n + 16);
+    uint8_t *d_out = (uint8_t *)honu_device_alloc(cap);
+    NEED(d_off && d_st && d_out);
+    CHECK(honu_marshal_batch(ctx, (const honu_meta *)d_rows, (const uint8_t *)d_var, tot[0],
+                             (const honu_acl *)d_acl, tot[1], (const uint32_t *)d_reg, tot[2],
+                             (const uint8_t *)d_pay, (const uint64_t *)d_poff, n, d_out, cap,
+                             d_off, d_st, NULL));
+    uint64_t *off = (uint64_t *)honu_host_alloc(8 * (n + 1));
+    int32_t *st = (int32_t *)honu_host_alloc(4 * n + 16);
+    NEED(off && st);
+    CHECK(honu_memcpy_d2h(off, d_off, 8 * (n + 1), NULL));
+    CHECK(honu_memcpy_d2h(st, d_st, 4 * n, NULL));
+    CHECK(honu_stream_sync(NULL));
+    for (uint64_t i = 0; i < n; i++)
+        if (st[i] != HONU_OK) {
+            fprintf(stderr, "record %llu: marshal status %d\n", (unsigned long long)i, st[i]);
+            return 1;
+        }
+    const uint64_t rec_bytes = off[n];
+    /* 4. Metadata() + zero-copy Data(), then a materialising decode */
+    honu_meta *d_meta = (honu_meta *)honu_device_alloc(sizeof(honu_meta) * n);
+    honu_record_info *d_info = (honu_record_info *)honu_device_alloc(sizeof(honu_record_info) * n);
+    honu_acl *d_tacl = (honu_acl *)honu_device_alloc(sizeof(honu_acl) * rec_bytes + 16);
+    uint32_t *d_treg = (uint32_t *)honu_device_alloc(4 * rec_bytes + 16);
+    uint64_t *d_tot = (uint64_t *)honu_device_alloc(32);
+    const uint64_t data_cap = rec_bytes + 16 * n;
+    uint8_t *d_data = (uint8_t *)honu_device_alloc(data_cap);
+    NEED(d_meta && d_info && d_tacl && d_treg && d_tot && d_data);
+    CHECK(honu_decode_batch(ctx, d_out, d_off, n, d_meta, d_info, d_tacl, rec_bytes, d_treg,
+                            rec_bytes, NULL, 0, d_tot, NULL));
+    honu_meta *meta = (honu_meta *)honu_host_alloc(sizeof(honu_meta) * n);
+    honu_record_info *info = (honu_record_info *)honu_host_alloc(sizeof(honu_record_info) * n);
+    NEED(meta && info);
+    CHECK(honu_memcpy_d2h(meta, d_meta, sizeof(honu_meta) * n, NULL));
+    CHECK(honu_memcpy_d2h(info, d_info, sizeof(honu_record_info) * n, NULL));
+    CHECK(honu_stream_sync(NULL));
+    for (uint64_t i = 0; i < n; i++) {
+        const honu_meta *a = rows + i, *b = meta + i;
+        if (info[i].meta_status != HONU_OK || info[i].data_status != HONU_OK ||
+            info[i].data_len != poff[i + 1] - poff[i] || a->pid != b->pid || a->vid != b->vid ||
+            a->created != b->created || a->modified != b->modified || a->acl_count != b->acl_count ||
+            a->regions_count != b->regions_count || memcmp(a->owner, b->owner, 16) != 0) {
+            fprintf(stderr, "record %llu: decoded fields differ (meta %d data %d)\n",
+                    (unsigned long long)i, info[i].meta_status, info[i].data_status);
+            return 1;
+        }
+    }
+    CHECK(honu_decode_batch(ctx, d_out, d_off, n, d_meta, d_info, d_tacl, rec_bytes, d_treg,
+                            rec_bytes, d_data, data_cap, d_tot, NULL));
+    uint8_t *data = (uint8_t *)honu_host_alloc(data_cap);
+    NEED(data);
+    CHECK(honu_memcpy_d2h(info, d_info, sizeof(honu_record_info) * n, NULL));
+    CHECK(honu_memcpy_d2h(data, d_data, data_cap, NULL));
+    CHECK(honu_stream_sync(NULL));
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t len = poff[i + 1] - poff[i];
+        if (info[i].data_len != len ||
+            honu_digest_host(data + info[i].data_off, len) != honu_digest_host(pay + poff[i], len)) {
+            fprintf(stderr, "record %llu: payload differs\n", (unsigned long long)i);
+            return 1;
+        }
+    }
+    printf("ok: %llu records, %llu encoded bytes, marshal + decode + materialise through the C ABI\n",
+           (unsigned long long)n, (unsigned long long)rec_bytes);
+    honu_ctx_destroy(ctx);
+    return 0;
+}
