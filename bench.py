@@ -10,10 +10,13 @@ fit one MI355X (≈197.6 GB of payload, ≈395 GB per direction pair), so the ba
 is processed as device-resident chunks of --chunk records whose output buffers
 are reused; every byte of every record is encoded and decoded each step.
 
-Multi-GPU: weak scaling, one process per GPU (torchrun), each rank encodes and
-decodes its own shard of --records records (records are independent: no
-data-path collective). A barrier + synchronize brackets the timed steps and the
-max time over ranks is reported.
+Multi-GPU: weak scaling, one process per GPU, each rank encodes and decodes its
+own shard of --records records (records are independent: no data-path
+collective). `--gpus N` without a torchrun environment spawns the N ranks itself
+(before anything touches the GPU) and fails if fewer than N devices are
+visible; under torchrun WORLD_SIZE must equal --gpus. A barrier + synchronize
+brackets the timed steps and the max time over ranks is reported; byte and
+record totals are summed over ranks.
 
 Prints ONE JSON line on rank 0 (see DESIGN.md for every field).
 """
@@ -22,6 +25,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,9 +45,12 @@ METRIC = "GiB/s + records/s device-resident encode+decode, 1M Large(~300KB) obje
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
-def parse_args():
+def parse_args(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="ranks (one per GPU); without torchrun the ranks are spawned here")
+    p.add_argument("--dry-run", action="store_true",
+                   help="stop before any device work: ranks report their shard (launcher test)")
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--records", type=int, default=1 << 20, help="records per GPU")
@@ -72,7 +80,7 @@ def parse_args():
                         "its header/tail encoder too")
     p.add_argument("--copy-blocks", type=int, default=0,
                    help="workgroups per CU of the payload copy engine (0 = library default)")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 def P(t):
@@ -178,6 +186,7 @@ class Bench:
         # payload copies: the bandwidth-bound critical path, dispatched first
         self.sc = (torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio else 0)
                    if nslots == 2 else self.sm)
+        self.sv = torch.cuda.Stream(self.dev)  # verification of drained chunks
         self.events = None
         self.last = None
         self.nchunk = 0  # chunks issued so far, across steps: slots alternate globally
@@ -198,108 +207,127 @@ class Bench:
         offsets and statuses (sizes + scan): it writes the payload bytes, the
         metadata kernels write only the bytes around them (byte-exact stores at
         the shared 16-byte chunks), so it runs beside the header/tail encoder.
-        check(a, b, slot) -> bool, when given, runs after each chunk completes
-        (verification pass); the result is the AND of its answers."""
+
+        check(a, b, slot) -> bool, when given, is called for chunk k once chunk
+        k+1 has been issued (so chunks still overlap exactly as in the timed
+        steps) and chunk k's slot has drained; it runs on its own stream and
+        must finish before it returns (chunk k+2 reuses the slot). The result
+        is the AND of its answers."""
+        ok = True
+        pending = None
+        for a, b in self.chunks:
+            sl = self._issue(a, b, timed)
+            if check is not None:
+                if pending is not None:
+                    ok &= self._check(check, pending)
+                pending = (a, b, sl)
+        if pending is not None:
+            ok &= self._check(check, pending)
+        torch.cuda.current_stream(self.dev).wait_stream(self.sc)
+        torch.cuda.current_stream(self.dev).wait_stream(self.sm)
+        return ok
+
+    def _check(self, check, pending):
+        a, b, sl = pending
+        sl.free.synchronize()  # chunk k's last copy done; chunk k+1 may still run
+        with torch.cuda.stream(self.sv):
+            return bool(check(a, b, sl))
+
+    def _issue(self, a, b, timed):
+        """Enqueue encode + materialising decode of records [a, b) into the
+        next slot; returns the slot."""
         L = self.lib
         sm, sc = self.sm, self.sc
-        ok = True
-        for k, (a, b) in enumerate(self.chunks):
-            n = b - a
-            # the slot after the previous chunk's, also across steps, so a
-            # step's first chunk overlaps the previous step's last one
-            sl = self.slots[self.nchunk % len(self.slots)]
-            self.nchunk += 1
-            c = sl.codec.ctx
-            if sl.free is not None:
-                sm.wait_event(sl.free)
-            ms = sm.cuda_stream
-            self._sizes(sl.codec, a, b, sl.out_off, sl.status, ms)
+        n = b - a
+        # the slot after the previous chunk's, also across steps, so a step's
+        # first chunk overlaps the previous step's last one
+        sl = self.slots[self.nchunk % len(self.slots)]
+        self.nchunk += 1
+        c = sl.codec.ctx
+        if sl.free is not None:
+            sm.wait_event(sl.free)
+        ms = sm.cuda_stream
+        self._sizes(sl.codec, a, b, sl.out_off, sl.status, ms)
+        ev_off = torch.cuda.Event()
+        ev_off.record(sm)
+        _lib.check(L.honu_encode_records(c, P(self.meta) + 352 * a, P(self.var), P(self.acl),
+                                         P(self.reg), P(self.off) + 8 * a, n, P(sl.out),
+                                         self.out_cap, P(sl.out_off), P(sl.status), ms),
+                   "encode_records")
+        if self.args.encode_copy_after == "meta":
             ev_off = torch.cuda.Event()
             ev_off.record(sm)
-            _lib.check(L.honu_encode_records(c, P(self.meta) + 352 * a, P(self.var), P(self.acl),
-                                             P(self.reg), P(self.off) + 8 * a, n, P(sl.out),
-                                             self.out_cap, P(sl.out_off), P(sl.status), ms),
-                       "encode_records")
-            if self.args.encode_copy_after == "meta":
-                ev_off = torch.cuda.Event()
-                ev_off.record(sm)
-            _lib.check(L.honu_decode_parse(c, P(sl.out), P(sl.out_off), n, P(sl.dmeta),
-                                           P(sl.dinfo), ms), "decode_parse")
-            _lib.check(L.honu_decode_tables(c, P(sl.out), n, P(sl.dmeta), P(sl.dinfo),
-                                            P(sl.dacl), self.acl_cap, P(sl.dreg), self.reg_cap,
-                                            P(sl.data), self.data_cap, P(sl.totals), ms),
-                       "decode_tables")
-            ev_fill = torch.cuda.Event()
-            ev_fill.record(sm)
-            cs = sc.cuda_stream
-            sc.wait_event(ev_off)
-            e0 = torch.cuda.Event(enable_timing=True) if timed else None
-            e1 = torch.cuda.Event(enable_timing=True) if timed else None
-            if timed:
-                e0.record(sc)
-            _lib.check(L.honu_encode_payloads(c, P(self.payload), P(self.off) + 8 * a, n,
-                                              P(sl.out), P(sl.out_off), P(sl.status), cs),
-                       "encode_payloads")
-            if timed:
-                e1.record(sc)
-            sc.wait_event(ev_fill)
-            e2 = torch.cuda.Event(enable_timing=True) if timed else None
-            e3 = torch.cuda.Event(enable_timing=True) if timed else None
-            if timed:
-                e2.record(sc)
-            _lib.check(L.honu_decode_payloads(c, P(sl.out), n, P(sl.dinfo), P(sl.data),
-                                              P(sl.totals), cs), "decode_payloads")
-            if timed:
-                e3.record(sc)
-                self.events.append((a, b, e0, e1, e2, e3))
-            sl.free = torch.cuda.Event()
-            sl.free.record(sc)
-            self.last = (a, b, sl)
-            if check is not None:
-                torch.cuda.synchronize()
-                ok &= check(a, b, sl)
-        torch.cuda.current_stream(self.dev).wait_stream(sc)
-        torch.cuda.current_stream(self.dev).wait_stream(sm)
-        return ok
+        _lib.check(L.honu_decode_parse(c, P(sl.out), P(sl.out_off), n, P(sl.dmeta),
+                                       P(sl.dinfo), ms), "decode_parse")
+        _lib.check(L.honu_decode_tables(c, P(sl.out), n, P(sl.dmeta), P(sl.dinfo),
+                                        P(sl.dacl), self.acl_cap, P(sl.dreg), self.reg_cap,
+                                        P(sl.data), self.data_cap, P(sl.totals), ms),
+                   "decode_tables")
+        ev_fill = torch.cuda.Event()
+        ev_fill.record(sm)
+        cs = sc.cuda_stream
+        sc.wait_event(ev_off)
+        e0 = torch.cuda.Event(enable_timing=True) if timed else None
+        e1 = torch.cuda.Event(enable_timing=True) if timed else None
+        if timed:
+            e0.record(sc)
+        _lib.check(L.honu_encode_payloads(c, P(self.payload), P(self.off) + 8 * a, n,
+                                          P(sl.out), self.out_cap, P(sl.out_off), P(sl.status),
+                                          cs), "encode_payloads")
+        if timed:
+            e1.record(sc)
+        sc.wait_event(ev_fill)
+        e2 = torch.cuda.Event(enable_timing=True) if timed else None
+        e3 = torch.cuda.Event(enable_timing=True) if timed else None
+        if timed:
+            e2.record(sc)
+        _lib.check(L.honu_decode_payloads(c, P(sl.out), n, P(sl.dinfo), P(sl.data),
+                                          P(sl.totals), cs), "decode_payloads")
+        if timed:
+            e3.record(sc)
+            self.events.append((a, b, e0, e1, e2, e3))
+        sl.free = torch.cuda.Event()
+        sl.free.record(sc)
+        self.last = (a, b, sl)
+        return sl
 
     def verify(self):
         """Every record of the batch, after the timed steps: one more pipelined
         step (same streams, slots and overlap as the timed ones) whose chunks
-        are each checked when complete by size-independent properties: every
-        encode and decode status is OK, every decoded payload's length and
-        position-aware digest equal its source's, and the decoded rows equal
-        the generator's input rows."""
+        are each checked once drained (_verify_chunk)."""
         torch.cuda.synchronize()
-        s = torch.cuda.current_stream(self.dev).cuda_stream
-        return bool(self.step(check=lambda a, b, sl: self._verify_chunk(a, b, sl, s)))
+        return bool(self.step(check=self._verify_chunk))
 
-    def _verify_chunk(self, a, b, sl, s):
+    VERIFIED_SCOPE = ("every record of every rank: encode and decode statuses; every decoded "
+                      "row byte against the source row (scalars, ULIDs, presence bits, span "
+                      "lengths and span bytes, ACL entries, regions; honu_verify_decoded); "
+                      "payload lengths + position-aware digests")
+
+    def _verify_chunk(self, a, b, sl):
+        """Chunk [a, b) as the pipeline left it in slot sl, on the current
+        (verification) stream: encode statuses OK; honu_verify_decoded of every
+        decoded row, span, ACL entry and region against the source row it was
+        encoded from; every materialised payload's digest equal to its
+        source's."""
         L, c = self.lib, sl.codec.ctx
         n = b - a
+        s = torch.cuda.current_stream(self.dev).cuda_stream
         st = sl.status[: 4 * n].view(torch.int32)
         info = sl.dinfo[: 32 * n].view(torch.int64).view(n, 4)
-        # data_status, meta_status pairs ((n, 1) int64 -> (n, 2) int32; the
-        # reshape keeps the last stride 1 even for a one-record chunk)
-        ms = info[:, 2].reshape(n, 1).contiguous().view(torch.int32)
+        mism = torch.empty(4 * n, dtype=torch.uint8, device=self.dev)
+        _lib.check(L.honu_verify_decoded(c, P(self.meta) + 352 * a, P(self.var), P(self.acl),
+                                         P(self.reg), P(self.off) + 8 * a, P(sl.out), P(sl.dmeta),
+                                         P(sl.dinfo), P(sl.dacl), P(sl.dreg), n, P(mism), s),
+                   "verify_decoded")
         dsrc = torch.empty(8 * n, dtype=torch.uint8, device=self.dev)
         ddst = torch.empty(8 * n, dtype=torch.uint8, device=self.dev)
         _lib.check(L.honu_digest_records(c, P(self.payload), P(self.off) + 8 * a, 0, n, P(dsrc), s),
                    "digest")
         doff, dlen = info[:, 0].contiguous(), info[:, 1].contiguous()
         _lib.check(L.honu_digest_records(c, P(sl.data), P(doff), P(dlen), n, P(ddst), s), "digest")
-        torch.cuda.synchronize()
-        ok = bool((st == 0).all()) and bool((ms == 0).all())
+        ok = bool((st == 0).all()) and int(torch.count_nonzero(mism.view(torch.int32))) == 0
         ok &= torch.equal(dsrc, ddst)
-        exp_len = torch.from_numpy(np.diff(self.host_off[a:b + 1].astype(np.int64))).to(self.dev)
-        ok &= torch.equal(dlen, exp_len)
-        rows = sl.dmeta[: 352 * n].cpu().numpy().view(self.host_meta.dtype)
-        src = self.host_meta[a:b]
-        for f in ("present", "pid", "vid", "region", "created", "modified", "acl_count",
-                  "regions_count", "permissions", "flags", "owner", "group"):
-            got, exp = rows[f], src[f]
-            if f == "present":  # decode adds REGIONS_NONNIL
-                got = got & ~np.uint32(0x80)
-            ok &= bool(np.array_equal(got, exp))
+        torch.cuda.current_stream(self.dev).synchronize()
         return bool(ok)
 
     def zero_copy_decode(self, reps=10):
@@ -429,11 +457,79 @@ def cpu_baseline(args):
     }
 
 
-def main():
-    args = parse_args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch(args, argv):
+    """--gpus N outside torchrun: start N ranks (this file again, one process
+    per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set) and return the first
+    failing exit code. Nothing here touches the GPU (device_count() only
+    counts), so the children own their devices from the start."""
+    n = args.gpus
+    if not args.dry_run:
+        visible = torch.cuda.device_count()
+        if visible < n:
+            print(f"bench.py: --gpus {n} needs {n} GPUs, {visible} visible", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:  # a rank that fails would leave the others blocked in a collective
+        for p in list(live):
+            if p.poll() is not None:
+                live.remove(p)
+                if p.returncode and not rc:
+                    rc = p.returncode
+                    for q in live:
+                        q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
+def dry_run(args, world, rank):
+    """The launcher's rank plumbing without device work: every rank reports
+    its weak-scaling shard over a gloo group; rank 0 prints them."""
+    first, n = weak_range(rank, world, args.records)
+    shards = [[rank, first, n]]
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        out = [None] * world
+        dist.all_gather_object(out, [rank, first, n, os.getpid()])
+        shards = out
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "ranks": world, "shards": shards}), flush=True)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch(args, argv))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        dry_run(args, world, rank)
+        return
+    if local >= torch.cuda.device_count():
+        print(f"bench.py: rank {rank} needs GPU {local}, {torch.cuda.device_count()} visible",
+              file=sys.stderr)
+        sys.exit(2)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -458,10 +554,20 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    # whole-job totals: every rank encodes/decodes its own records
+    per_rank_s = [elapsed]
+    tot = [bench.total_rec_bytes, bench.N]
+    ranks, backend = 1, None
     if dist is not None:
+        ranks, backend = dist.get_world_size(), dist.get_backend()
         t = torch.tensor([elapsed], dtype=torch.float64, device=bench.dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        gathered = [torch.zeros_like(t) for _ in range(ranks)]
+        dist.all_gather(gathered, t)
+        per_rank_s = [float(x.item()) for x in gathered]
+        elapsed = max(per_rank_s)
+        tt = torch.tensor(tot, dtype=torch.int64, device=bench.dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        tot = [int(x) for x in tt.tolist()]
 
     # per-launch kernel times of the two payload-copy kernels (the HBM-bound part)
     enc_ms = [e0.elapsed_time(e1) for (_, _, e0, e1, _, _) in bench.events]
@@ -482,8 +588,7 @@ def main():
             dist.destroy_process_group()
         return
     step_s = elapsed / args.steps
-    total_records = bench.N * world
-    total_bytes = bench.total_rec_bytes * world
+    total_bytes, total_records = tot
     launches = len(dec_ms)
     dom_ms, dom_gbs, dom_name = (sum(dec_ms), dec_gbs, "k_copy_segments<honu::DecodeSegments>")
     if sum(enc_ms) > sum(dec_ms):
@@ -528,6 +633,11 @@ def main():
             "copy_blocks_per_cu": args.copy_blocks or 2,
         },
         "records_per_s": total_records / step_s,
+        "ranks": ranks,
+        "backend": backend,
+        "per_rank_ms_per_step": [x / args.steps * 1e3 for x in per_rank_s],
+        "encoded_bytes_all_ranks": total_bytes,
+        "records_all_ranks": total_records,
         "roofline": {
             "bound": "hbm",
             "kernel": dom_name,
@@ -553,8 +663,7 @@ def main():
             "zero_copy_decode_chunk_records": zc["records"],
         },
         "verified": ok_all,
-        "verified_scope": None if ok_all is None else
-        "every record of every rank: statuses, payload lengths + digests, decoded rows vs input rows",
+        "verified_scope": None if ok_all is None else Bench.VERIFIED_SCOPE,
     }
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)

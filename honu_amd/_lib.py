@@ -37,7 +37,7 @@ _PROTOS = {
     "honu_exclusive_scan": (I32, [P, P, U64, P, P]),
     "honu_encode": (I32, [P, P, P, U64, P, U64, P, U64, P, P, U64, P, U64, P, P, P]),
     "honu_encode_records": (I32, [P, P, P, P, P, P, U64, P, U64, P, P, P]),
-    "honu_encode_payloads": (I32, [P, P, P, U64, P, P, P, P]),
+    "honu_encode_payloads": (I32, [P, P, P, U64, P, U64, P, P, P]),
     "honu_decode_tables": (I32, [P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),
     "honu_decode_payloads": (I32, [P, P, U64, P, P, P, P]),
     "honu_marshal_batch": (I32, [P, P, P, U64, P, U64, P, U64, P, P, U64, P, U64, P, P, P]),
@@ -54,6 +54,7 @@ _PROTOS = {
     "honu_system_marshal_batch": (I32, [P, P, P, U64, P, U64, P, U64, P, U64, U64, P, U64, P, P,
                                         P]),
     "honu_system_decode_batch": (I32, [P, P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),
+    "honu_collection_decode_batch": (I32, [P, P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),
     "honu_feed_create": (P, [C.c_int, U64, U64, C.c_uint32, C.POINTER(I32)]),
     "honu_feed_destroy": (None, [P]),
     "honu_feed_append": (I32, [P, P, U64]),
@@ -75,6 +76,7 @@ _PROTOS = {
     "honu_gen_payload": (I32, [P, U64, U64, U64, P, P, P]),
     "honu_digest_records": (I32, [P, P, P, P, U64, P, P]),
     "honu_digest_host": (U64, [P, U64]),
+    "honu_verify_decoded": (I32, [P, P, P, P, P, P, P, P, P, P, P, U64, P, P]),
     "honu_host_alloc": (P, [U64]),
     "honu_host_free": (None, [P]),
     "honu_device_alloc": (P, [U64]),

@@ -231,13 +231,13 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
 }
 
 int32_t honu_encode_payloads(honu_ctx *ctx, const uint8_t *d_payload, const uint64_t *d_payload_off,
-                             uint64_t n, uint8_t *d_out, const uint64_t *d_out_off,
+                             uint64_t n, uint8_t *d_out, uint64_t out_cap, const uint64_t *d_out_off,
                              const int32_t *d_status, void *stream) {
     if (!ctx) return arg_fail("ctx");
     if (n && (!d_payload_off || !d_out || !d_out_off || !d_status)) return arg_fail("null pointer");
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(launch_encode_copy(ctx->geom, d_payload, d_payload_off, n, d_out, d_out_off, d_status,
-                              (hipStream_t)stream));
+    HIPCHK(launch_encode_copy(ctx->geom, d_payload, d_payload_off, n, d_out, out_cap, d_out_off,
+                              d_status, (hipStream_t)stream));
     return HONU_OK;
 }
 
@@ -252,8 +252,8 @@ int32_t honu_encode(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var
     int32_t st = honu_encode_records(ctx, d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
                                      out_cap, d_out_off, d_status, stream);
     if (st) return st;
-    return honu_encode_payloads(ctx, d_payload, d_payload_off, n, d_out, d_out_off, d_status,
-                                stream);
+    return honu_encode_payloads(ctx, d_payload, d_payload_off, n, d_out, out_cap, d_out_off,
+                                d_status, stream);
 }
 
 int32_t honu_marshal_batch(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
@@ -477,11 +477,11 @@ int32_t honu_system_marshal_batch(honu_ctx *ctx, const honu_collection *d_rows,
                               d_out_off, d_status, stream);
 }
 
-int32_t honu_system_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
-                                 uint64_t n, honu_collection *d_rows, int32_t *d_status,
-                                 honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
-                                 uint64_t regions_cap, honu_index *d_index, uint64_t index_cap,
-                                 uint64_t *d_totals, void *stream) {
+static int32_t collection_decode(honu_ctx *ctx, bool headless, const uint8_t *d_rec,
+                                 const uint64_t *d_rec_off, uint64_t n, honu_collection *d_rows,
+                                 int32_t *d_status, honu_acl *d_acl, uint64_t acl_cap,
+                                 uint32_t *d_regions, uint64_t regions_cap, honu_index *d_index,
+                                 uint64_t index_cap, uint64_t *d_totals, void *stream) {
     if (!ctx) return arg_fail("ctx");
     if (n > ctx->max_n) return HONU_E_WORKSPACE;
     if (n && (!d_rec || !d_rec_off || !d_rows || !d_status)) return arg_fail("null pointer");
@@ -493,12 +493,31 @@ int32_t honu_system_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     uint64_t *tot = d_totals ? d_totals : ctx->totals;
-    HIPCHK(launch_system_parse(d_rec, d_rec_off, n, d_rows, d_status, ctx->scratch, ctx->counts,
-                               s));
+    HIPCHK(launch_system_parse(d_rec, d_rec_off, n, headless, d_rows, d_status, ctx->scratch,
+                               ctx->counts, s));
     HIPCHK(launch_scan(ctx->counts, n, 3, ctx->offs, tot, ctx->partials, s));
     HIPCHK(launch_system_fill(d_rec, n, d_rows, d_status, ctx->scratch, ctx->counts, ctx->offs,
                               d_acl, acl_cap, d_regions, regions_cap, d_index, index_cap, s));
     return HONU_OK;
+}
+
+int32_t honu_system_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                                 uint64_t n, honu_collection *d_rows, int32_t *d_status,
+                                 honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
+                                 uint64_t regions_cap, honu_index *d_index, uint64_t index_cap,
+                                 uint64_t *d_totals, void *stream) {
+    return collection_decode(ctx, false, d_rec, d_rec_off, n, d_rows, d_status, d_acl, acl_cap,
+                             d_regions, regions_cap, d_index, index_cap, d_totals, stream);
+}
+
+int32_t honu_collection_decode_batch(honu_ctx *ctx, const uint8_t *d_rec,
+                                     const uint64_t *d_rec_off, uint64_t n,
+                                     honu_collection *d_rows, int32_t *d_status, honu_acl *d_acl,
+                                     uint64_t acl_cap, uint32_t *d_regions, uint64_t regions_cap,
+                                     honu_index *d_index, uint64_t index_cap, uint64_t *d_totals,
+                                     void *stream) {
+    return collection_decode(ctx, true, d_rec, d_rec_off, n, d_rows, d_status, d_acl, acl_cap,
+                             d_regions, regions_cap, d_index, index_cap, d_totals, stream);
 }
 
 // ---------------------------------------------------------------------------
@@ -518,6 +537,22 @@ int32_t honu_digest_records(honu_ctx *ctx, const uint8_t *d_arena, const uint64_
     if (!ctx) return arg_fail("ctx");
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(launch_digest(ctx->geom, d_arena, d_off, d_len, n, d_digest, (hipStream_t)stream));
+    return HONU_OK;
+}
+
+int32_t honu_verify_decoded(honu_ctx *ctx, const honu_meta *d_src, const uint8_t *d_var,
+                            const honu_acl *d_src_acl, const uint32_t *d_src_regions,
+                            const uint64_t *d_payload_off, const uint8_t *d_rec,
+                            const honu_meta *d_dec, const honu_record_info *d_info,
+                            const honu_acl *d_dec_acl, const uint32_t *d_dec_regions, uint64_t n,
+                            uint32_t *d_mismatch, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n && (!d_src || !d_payload_off || !d_rec || !d_dec || !d_info || !d_mismatch))
+        return arg_fail("null pointer");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_verify_decoded(ctx->geom, d_src, d_var, d_src_acl, d_src_regions, d_payload_off,
+                                 d_rec, d_dec, d_info, d_dec_acl, d_dec_regions, n, d_mismatch,
+                                 (hipStream_t)stream));
     return HONU_OK;
 }
 

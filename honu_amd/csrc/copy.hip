@@ -24,6 +24,7 @@ struct EncodeSegments {
     const uint8_t *payload;
     const uint64_t *payload_off;
     uint8_t *out;
+    uint64_t out_cap;
     const uint64_t *out_off;
     const int32_t *status;
 
@@ -34,7 +35,10 @@ struct EncodeSegments {
         return payload_off[i + 1];
     }
     HONU_DEV bool get(uint64_t i, uint64_t &len, const uint8_t *&src, uint8_t *&dst) const {
-        if (status[i] != HONU_OK) return false;
+        // the header/tail encoder may still be running on another stream:
+        // its HONU_ERR_CAPACITY is not visible here, so the capacity check
+        // is repeated (nothing is written past out_cap)
+        if (status[i] != HONU_OK || out_off[i + 1] > out_cap) return false;
         const uint64_t s = payload_off[i];
         len = payload_off[i + 1] - s;
         src = payload + s;
@@ -215,9 +219,10 @@ static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
 
 hipError_t launch_encode_copy(const LaunchGeom &g, const uint8_t *payload,
                               const uint64_t *payload_off, uint64_t n, uint8_t *out,
-                              const uint64_t *out_off, const int32_t *status, hipStream_t s) {
+                              uint64_t out_cap, const uint64_t *out_off, const int32_t *status,
+                              hipStream_t s) {
     if (n == 0) return hipSuccess;
-    EncodeSegments seg{payload, payload_off, out, out_off, status};
+    EncodeSegments seg{payload, payload_off, out, out_cap, out_off, status};
     return launch_copy(g, seg, n, payload_off + n, s);
 }
 

@@ -296,9 +296,14 @@ int32_t honu_feed_wait(honu_feed *f, uint64_t ticket, honu_feed_result *out) {
     out->meta = hdr ? nullptr : s.h_meta;
     out->info = s.h_info;
     out->acl = hdr ? nullptr : s.h_acl;
-    out->acl_n = hdr ? 0 : s.h_tot[0];
+    // the tables hold at most acl_cap / reg_cap entries; a batch that needs
+    // more (nil-entry floods) reports its need separately, so a binding that
+    // slices acl[0:acl_n] never reads past the pinned allocation
+    out->acl_n = hdr ? 0 : (s.h_tot[0] < f->acl_cap ? s.h_tot[0] : f->acl_cap);
     out->regions = hdr ? nullptr : s.h_reg;
-    out->regions_n = hdr ? 0 : s.h_tot[1];
+    out->regions_n = hdr ? 0 : (s.h_tot[1] < f->reg_cap ? s.h_tot[1] : f->reg_cap);
+    out->acl_needed = hdr ? 0 : s.h_tot[0];
+    out->regions_needed = hdr ? 0 : s.h_tot[1];
     out->keys = hdr ? nullptr : s.h_keys;
     out->key_status = hdr ? nullptr : s.h_kst;
     return HONU_OK;

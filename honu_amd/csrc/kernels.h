@@ -71,7 +71,8 @@ hipError_t launch_encode_meta(const LaunchGeom &g, const honu_meta *meta, const 
                               hipStream_t s);
 hipError_t launch_encode_copy(const LaunchGeom &g, const uint8_t *payload,
                               const uint64_t *payload_off, uint64_t n, uint8_t *out,
-                              const uint64_t *out_off, const int32_t *status, hipStream_t s);
+                              uint64_t out_cap, const uint64_t *out_off, const int32_t *status,
+                              hipStream_t s);
 
 hipError_t launch_decode_parse(const LaunchGeom &g, const uint8_t *rec, const uint64_t *rec_off,
                                uint64_t n, honu_meta *meta, honu_record_info *info,
@@ -146,8 +147,8 @@ hipError_t launch_system_encode(const honu_collection *rows, const uint8_t *var,
                                 uint64_t n, uint8_t *out, uint64_t out_cap,
                                 const uint64_t *out_off, int32_t *status, hipStream_t s);
 hipError_t launch_system_parse(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
-                               honu_collection *rows, int32_t *status, DecodeScratch *scratch,
-                               uint64_t *counts, hipStream_t s);
+                               bool headless, honu_collection *rows, int32_t *status,
+                               DecodeScratch *scratch, uint64_t *counts, hipStream_t s);
 hipError_t launch_system_fill(const uint8_t *rec, uint64_t n, honu_collection *rows,
                               int32_t *status, const DecodeScratch *scratch,
                               const uint64_t *counts, const uint64_t *offs, honu_acl *acl,
@@ -173,6 +174,12 @@ hipError_t launch_scan(const uint64_t *in, uint64_t n, int K, uint64_t *out, uin
 
 hipError_t launch_gen_payload(const LaunchGeom &g, uint64_t seed, uint64_t first, uint64_t n,
                               const uint64_t *payload_off, uint8_t *payload, hipStream_t s);
+hipError_t launch_verify_decoded(const LaunchGeom &g, const honu_meta *src, const uint8_t *var,
+                                 const honu_acl *src_acl, const uint32_t *src_reg,
+                                 const uint64_t *payload_off, const uint8_t *rec,
+                                 const honu_meta *dec, const honu_record_info *info,
+                                 const honu_acl *dec_acl, const uint32_t *dec_reg, uint64_t n,
+                                 uint32_t *mismatch, hipStream_t s);
 hipError_t launch_digest(const LaunchGeom &g, const uint8_t *arena, const uint64_t *off,
                          const uint64_t *len, uint64_t n, uint64_t *digest, hipStream_t s);
 

@@ -88,6 +88,116 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_digest(const uint8_t *__restrict
     }
 }
 
+
+// ------------------------------------------------------------------------
+// Round-trip check of a decoded batch against the rows it was encoded from
+// (honu_verify_decoded). One wave per record; every byte of the 352-byte row
+// is compared with the value the Go decoder must produce from the source
+// row: the source byte when the field's struct is present, zero when it is
+// nil (fields of nil structs stay zero, metadata.go:202-302), REGIONS_NONNIL
+// added (region.go:160). Span offsets index different arenas and are not
+// compared; their bytes are. ACL entries and regions are compared entry by
+// entry through both rows' list offsets.
+// ------------------------------------------------------------------------
+constexpr uint32_t G_ALWAYS = 0, G_IGNORE = 0xFFFFFFFFu, G_ZERO = 0xFFFFFFFEu;
+
+// Presence bit that gates row byte b (G_ALWAYS: unconditional field,
+// G_ZERO: padding, G_IGNORE: not compared bytewise).
+HONU_DEV uint32_t row_gate(uint32_t b) {
+    if (b < 4) return G_IGNORE;  // present: checked as a whole
+    if (b < 6) return G_ALWAYS;  // permissions, flags
+    if (b == 6) return HONU_HAS_VERSION;  // tombstone
+    if (b == 7) return HONU_HAS_COMPRESSION;
+    if (b < 11) return HONU_HAS_ENCRYPTION;  // sealing/encryption/signature alg
+    if (b < 12) return G_ZERO;
+    if (b < 28) return HONU_HAS_VERSION;  // region, vid, pid
+    if (b < 40) return HONU_HAS_PARENT;
+    if (b < 48) return HONU_HAS_VERSION;  // version_created
+    if (b < 60) return HONU_HAS_SCHEMA;
+    if (b < 64) return G_ZERO;
+    if (b < 72) return HONU_HAS_COMPRESSION;
+    if (b < 88) return G_ALWAYS;  // created, modified
+    if (b < 96) return G_ZERO;
+    if (b < 160) return G_ALWAYS;  // object_id, collection_id, owner, group
+    if (b < 192) return HONU_HAS_PUBLISHER;
+    if (b < 320) {  // spans: offsets ignored, lengths gated
+        if ((b & 15) < 8) return G_IGNORE;
+        const uint32_t k = (b - 192) >> 4;  // schema_name, mime, ip, ua, 4 x encryption
+        return k == 0 ? HONU_HAS_SCHEMA : k == 1 ? G_ALWAYS : k < 4 ? HONU_HAS_PUBLISHER
+                                                             : HONU_HAS_ENCRYPTION;
+    }
+    if (b < 328 || (b >= 336 && b < 344)) return G_IGNORE;  // list offsets
+    return G_ALWAYS;  // acl_count, regions_count
+}
+
+// The presence bits the decoder reports for an encoded source row.
+HONU_DEV uint32_t decoded_present(uint32_t p) {
+    if (!(p & HONU_HAS_META)) return 0;
+    p &= 0x7Fu;
+    if (!(p & HONU_HAS_VERSION)) p &= ~(uint32_t)HONU_HAS_PARENT;  // Parent lives inside Version
+    return p | HONU_REGIONS_NONNIL;
+}
+
+__global__ __launch_bounds__(HONU_BLOCK) void k_verify_decoded(
+    const honu_meta *__restrict__ src, const uint8_t *__restrict__ var,
+    const honu_acl *__restrict__ src_acl, const uint32_t *__restrict__ src_reg,
+    const uint64_t *__restrict__ payload_off, const uint8_t *__restrict__ rec,
+    const honu_meta *__restrict__ dec, const honu_record_info *__restrict__ info,
+    const honu_acl *__restrict__ dec_acl, const uint32_t *__restrict__ dec_reg, uint64_t n,
+    uint32_t *__restrict__ mismatch) {
+    const uint64_t nwaves = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
+    const uint32_t lane = lane_id();
+    for (uint64_t i = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + wave_in_block(); i < n;
+         i += nwaves) {
+        const honu_meta &S = src[i], &D = dec[i];
+        const uint8_t *sb = reinterpret_cast<const uint8_t *>(&S);
+        const uint8_t *db = reinterpret_cast<const uint8_t *>(&D);
+        const uint32_t sp = S.present;
+        const uint32_t pr = decoded_present(sp);
+        const honu_record_info inf = info[i];
+        uint32_t bad = 0;
+        if (inf.data_status != HONU_OK || inf.meta_status != HONU_OK) bad |= HONU_VERIFY_STATUS;
+        if (inf.data_len != payload_off[i + 1] - payload_off[i]) bad |= HONU_VERIFY_STATUS;
+        if (D.present != pr) bad |= HONU_VERIFY_PRESENT;
+        bool row_bad = false;
+        for (uint32_t b = lane; b < sizeof(honu_meta); b += HONU_WAVE) {
+            const uint32_t g = row_gate(b);
+            if (g == G_IGNORE) continue;
+            const bool on = pr != 0 && (g == G_ALWAYS || (g != G_ZERO && (pr & g)));
+            if (db[b] != (on ? sb[b] : 0)) row_bad = true;
+        }
+        if (__ballot(row_bad)) bad |= HONU_VERIFY_FIELDS;
+        if (bad == 0 && pr) {
+            bool span_bad = false;
+            const honu_span *ss = &S.schema_name, *ds = &D.schema_name;
+            for (int k = 0; k < 8; k++) {
+                const uint64_t len = ds[k].len;  // equal to the source's (checked above)
+                for (uint64_t j = lane; j < len; j += HONU_WAVE)
+                    if (var[ss[k].off + j] != rec[ds[k].off + j]) span_bad = true;
+            }
+            if (__ballot(span_bad)) bad |= HONU_VERIFY_SPANS;
+            bool acl_bad = false;
+            for (uint64_t j = lane; j < S.acl_count; j += HONU_WAVE) {
+                const honu_acl &a = src_acl[S.acl_off + j], &e = dec_acl[D.acl_off + j];
+                const uint32_t *ew = reinterpret_cast<const uint32_t *>(&e);
+                const uint32_t *aw = reinterpret_cast<const uint32_t *>(&a);
+                if (a.present) {
+                    for (int q = 0; q < 4; q++) acl_bad |= ew[q] != aw[q];
+                    acl_bad |= ew[4] != (a.permissions | (1u << 8));
+                } else {
+                    for (int q = 0; q < 5; q++) acl_bad |= ew[q] != 0;
+                }
+            }
+            if (__ballot(acl_bad)) bad |= HONU_VERIFY_ACL;
+            bool reg_bad = false;
+            for (uint64_t j = lane; j < S.regions_count; j += HONU_WAVE)
+                reg_bad |= src_reg[S.regions_off + j] != dec_reg[D.regions_off + j];
+            if (__ballot(reg_bad)) bad |= HONU_VERIFY_REGIONS;
+        }
+        if (lane == 0) mismatch[i] = bad;
+    }
+}
+
 hipError_t launch_gen_payload(const LaunchGeom &g, uint64_t seed, uint64_t first, uint64_t n,
                               const uint64_t *payload_off, uint8_t *payload, hipStream_t s) {
     if (n == 0) return hipSuccess;
@@ -105,6 +215,21 @@ hipError_t launch_digest(const LaunchGeom &g, const uint8_t *arena, const uint64
     if (b > (uint64_t)g.per_record_blocks) b = g.per_record_blocks;
     hipLaunchKernelGGL(k_digest, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, arena, off, len, n,
                        digest);
+    return hipGetLastError();
+}
+
+hipError_t launch_verify_decoded(const LaunchGeom &g, const honu_meta *src, const uint8_t *var,
+                                 const honu_acl *src_acl, const uint32_t *src_reg,
+                                 const uint64_t *payload_off, const uint8_t *rec,
+                                 const honu_meta *dec, const honu_record_info *info,
+                                 const honu_acl *dec_acl, const uint32_t *dec_reg, uint64_t n,
+                                 uint32_t *mismatch, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    uint64_t b = (n + 3) / 4;
+    if (b > (uint64_t)g.per_record_blocks) b = g.per_record_blocks;
+    hipLaunchKernelGGL(k_verify_decoded, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, src, var,
+                       src_acl, src_reg, payload_off, rec, dec, info, dec_acl, dec_reg, n,
+                       mismatch);
     return hipGetLastError();
 }
 

@@ -291,29 +291,34 @@ HONU_DEV int skip_index(LaneDec &D) {
     return HONU_OK;
 }
 
+// headless = false: object.UnmarshalSystem(obj, &Collection{}) (system.go:36-45):
+// obj[1 : len-1], struct flag first. headless = true: lani.Unmarshal(obj,
+// &Collection{}) (lani.go:29-33) as store.go:367 calls it on a raw bbolt
+// value: Collection.Decode from byte 0 to the end, no flag.
 HONU_DEV void system_parse_one(uint64_t i, const uint8_t *__restrict__ rec,
-                               const uint64_t *__restrict__ rec_off,
+                               const uint64_t *__restrict__ rec_off, bool headless,
                                honu_collection *__restrict__ rows,
                                int32_t *__restrict__ status, DecodeScratch *__restrict__ scratch,
                                uint64_t *__restrict__ counts) {
     const uint64_t beg = rec_off[i], end = rec_off[i + 1];
+    const uint64_t t0 = headless ? beg : beg + 1, t1 = headless ? end : end - 1;
     CRow R;
     R.clear();
     uint64_t nacl = 0, nreg = 0, nidx = 0, acl_pos = 0, reg_pos = 0, idx_pos = 0;
     int st = HONU_OK;
-    if (end - beg < 2) {
+    if (!headless && end - beg < 2) {
         st = HONU_ERR_PANIC;  // obj[1 : len(obj)-1] out of range (system.go:40)
     } else {
         LaneDec D;
         D.base = rec;
-        D.tstart = beg + 1;
-        D.p = beg + 1;
-        D.end = end - 1;
-        uint32_t f, u;
+        D.tstart = t0;
+        D.p = t0;
+        D.end = t1;
+        uint32_t f = 1, u;
         uint64_t v, o, l, lo, hi;
         int64_t t;
         uint32_t pr = 0;
-        TRY(D.boolean(f));                                  // DecodeStruct(v) system.go:41
+        if (!headless) TRY(D.boolean(f));                   // DecodeStruct(v) system.go:41
         if (f) {
             pr = HONU_HAS_COLLECTION;
             TRY(D.ulid(lo, hi)); R.bytes16(COFF(id), lo, hi);          // collection.go:248
@@ -411,7 +416,7 @@ done:
     }
     R.store(rows + i);
     status[i] = st;
-    scratch[i] = DecodeScratch{acl_pos, reg_pos, idx_pos, end - 1};
+    scratch[i] = DecodeScratch{acl_pos, reg_pos, idx_pos, t1};
     counts[3 * i + 0] = nacl;
     counts[3 * i + 1] = nreg;
     counts[3 * i + 2] = nidx;
@@ -420,11 +425,11 @@ done:
 
 __global__ __launch_bounds__(HONU_BLOCK) void k_system_parse(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
-    honu_collection *__restrict__ rows, int32_t *__restrict__ status,
+    bool headless, honu_collection *__restrict__ rows, int32_t *__restrict__ status,
     DecodeScratch *__restrict__ scratch, uint64_t *__restrict__ counts) {
     for (uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * HONU_BLOCK)
-        system_parse_one(i, rec, rec_off, rows, status, scratch, counts);
+        system_parse_one(i, rec, rec_off, headless, rows, status, scratch, counts);
 }
 
 // Field.Decode into an index row (walk validated by the parse)
@@ -561,11 +566,11 @@ hipError_t launch_system_encode(const honu_collection *rows, const uint8_t *var,
 }
 
 hipError_t launch_system_parse(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
-                               honu_collection *rows, int32_t *status, DecodeScratch *scratch,
-                               uint64_t *counts, hipStream_t s) {
+                               bool headless, honu_collection *rows, int32_t *status,
+                               DecodeScratch *scratch, uint64_t *counts, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_system_parse, sys_grid(n), dim3(HONU_BLOCK), 0, s, rec, rec_off, n, rows,
-                       status, scratch, counts);
+    hipLaunchKernelGGL(k_system_parse, sys_grid(n), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
+                       headless, rows, status, scratch, counts);
     return hipGetLastError();
 }
 

@@ -21,7 +21,8 @@ class _Result(C.Structure):
     _fields_ = [("n", C.c_uint64), ("records", C.c_void_p), ("rec_off", C.c_void_p),
                 ("meta", C.c_void_p), ("info", C.c_void_p), ("acl", C.c_void_p),
                 ("acl_n", C.c_uint64), ("regions", C.c_void_p), ("regions_n", C.c_uint64),
-                ("keys", C.c_void_p), ("key_status", C.c_void_p)]
+                ("keys", C.c_void_p), ("key_status", C.c_void_p),
+                ("acl_needed", C.c_uint64), ("regions_needed", C.c_uint64)]
 
 
 def _view(ptr, count, dtype):
@@ -42,6 +43,8 @@ class FeedResult:
     regions: Optional[np.ndarray]
     keys: Optional[np.ndarray]   # (n, 29) uint8
     key_status: Optional[np.ndarray]
+    acl_needed: int = 0          # table entries the batch needed (> len(acl): overflow)
+    regions_needed: int = 0
 
 
 class RecordFeed:
@@ -107,7 +110,8 @@ class RecordFeed:
             None if hdr else _view(r.acl, r.acl_n, ACL_DTYPE),
             None if hdr else _view(r.regions, r.regions_n, np.uint32),
             None if hdr else _view(r.keys, 29 * n, np.uint8).reshape(n, 29),
-            None if hdr else _view(r.key_status, n, np.int32))
+            None if hdr else _view(r.key_status, n, np.int32),
+            int(r.acl_needed), int(r.regions_needed))
 
 
 # --------------------------------------------------------------------------

@@ -254,7 +254,7 @@ def marshal_system_batch(cols: Sequence[Optional[Collection]], codec=None):
             _to_host(st, 4 * n, np.int32))
 
 
-def decode_system_batch(rec: np.ndarray, rec_off: np.ndarray, codec=None):
+def decode_system_batch(rec: np.ndarray, rec_off: np.ndarray, codec=None, headless=False):
     """UnmarshalSystem(obj, &Collection{}) for a CSR batch on the GPU ->
     (rows, status, acl table, region table, index table, totals[3])."""
     from .object import _to_host, default_codec
@@ -271,9 +271,9 @@ def decode_system_batch(rec: np.ndarray, rec_off: np.ndarray, codec=None):
     idx = codec._empty(INDEX_DTYPE.itemsize * cap)
     tot = codec._empty(32)
     P = _lib.ptr
-    _lib.check(codec.lib.honu_system_decode_batch(
-        codec.ctx, P(d_rec), P(d_off), n, P(rows), P(st), P(acl), cap, P(reg), cap, P(idx), cap,
-        P(tot), codec.stream), "honu_system_decode_batch")
+    fn = codec.lib.honu_collection_decode_batch if headless else codec.lib.honu_system_decode_batch
+    _lib.check(fn(codec.ctx, P(d_rec), P(d_off), n, P(rows), P(st), P(acl), cap, P(reg), cap,
+                  P(idx), cap, P(tot), codec.stream), "honu collection decode")
     t = _to_host(tot, 24, np.uint64)
     return (_to_host(rows, COLLECTION_DTYPE.itemsize * n, COLLECTION_DTYPE),
             _to_host(st, 4 * n, np.int32), _to_host(acl, ACL_DTYPE.itemsize * int(t[0]), ACL_DTYPE),
@@ -296,6 +296,22 @@ def UnmarshalSystem(obj: bytes) -> Collection:
     from .object import _ERRORS, HonuCodecError
     rec = np.frombuffer(bytes(obj), np.uint8)
     rows, st, acl, reg, idx, _ = decode_system_batch(rec, np.array([0, len(obj)], np.uint64))
+    if st[0]:
+        raise _ERRORS.get(int(st[0]), HonuCodecError)(f"status {int(st[0])}")
+    return unpack_collection(rows[0], rec, acl, reg, idx)
+
+
+def Unmarshal(raw: bytes, c: Optional[Collection] = None) -> Collection:
+    """lani.Unmarshal(raw, c) with c a *metadata.Collection (lani/lani.go:29-33):
+    Collection.Decode from byte 0 of raw, as pkg/store calls it on raw bbolt
+    values (store.go:155, :367). c=None is store.go:155's nil pointer, on
+    which the reference panics (collection.go:242 assigns through it)."""
+    from .object import _ERRORS, GoPanic, HonuCodecError
+    if c is None:
+        raise GoPanic("Collection.Decode on a nil *Collection (store.go:155)")
+    rec = np.frombuffer(bytes(raw), np.uint8)
+    rows, st, acl, reg, idx, _ = decode_system_batch(rec, np.array([0, len(raw)], np.uint64),
+                                                     headless=True)
     if st[0]:
         raise _ERRORS.get(int(st[0]), HonuCodecError)(f"status {int(st[0])}")
     return unpack_collection(rows[0], rec, acl, reg, idx)

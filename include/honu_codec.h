@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define HONU_ABI_VERSION 2u
+#define HONU_ABI_VERSION 3u
 #define HONU_STORAGE_VERSION 1u /* object.StorageVersion, object.go:14 */
 #define HONU_ULID_LEN 16
 #define HONU_KEY_LEN 29         /* keys.keySize, keys/keys.go:14 */
@@ -252,9 +252,13 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
                             const uint64_t *d_payload_off, uint64_t n, uint8_t *d_out,
                             uint64_t out_cap, const uint64_t *d_out_off, int32_t *d_status,
                             void *stream);
+/* honu_encode_payloads needs only d_out_off and the size pass's d_status, so it
+ * may run on another stream beside honu_encode_records (each writes only its
+ * own bytes of the shared 16-byte chunks); it repeats the out_cap check
+ * itself and copies nothing for a record that ends past out_cap. */
 int32_t honu_encode_payloads(honu_ctx *ctx, const uint8_t *d_payload, const uint64_t *d_payload_off,
-                             uint64_t n, uint8_t *d_out, const uint64_t *d_out_off,
-                             const int32_t *d_status, void *stream);
+                             uint64_t n, uint8_t *d_out, uint64_t out_cap,
+                             const uint64_t *d_out_off, const int32_t *d_status, void *stream);
 
 /* sizes + scan + encode in one call; d_out_off (n+1) is produced here. */
 int32_t honu_marshal_batch(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
@@ -457,6 +461,21 @@ int32_t honu_system_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint
                                  honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
                                  uint64_t regions_cap, honu_index *d_index, uint64_t index_cap,
                                  uint64_t *d_totals, void *stream);
+/* lani.Unmarshal(raw, &metadata.Collection{}) (lani/lani.go:29-33) for n
+ * records: Collection.Decode (collection.go:240-356) from byte 0 of each raw
+ * value to its end, as the store calls it on the bbolt value of a system
+ * object (store.go:367, whose storage-version and struct-flag bytes are then
+ * read as the first bytes of the ID). Rows, tables and statuses as
+ * honu_system_decode_batch; a row that decodes has HONU_HAS_COLLECTION set
+ * (the target is never nil). store.go:155 passes a nil *Collection, on which
+ * Collection.Decode always panics (nil dereference, collection.go:242): no
+ * batch call is needed to reproduce that. */
+int32_t honu_collection_decode_batch(honu_ctx *ctx, const uint8_t *d_rec,
+                                     const uint64_t *d_rec_off, uint64_t n,
+                                     honu_collection *d_rows, int32_t *d_status, honu_acl *d_acl,
+                                     uint64_t acl_cap, uint32_t *d_regions, uint64_t regions_cap,
+                                     honu_index *d_index, uint64_t index_cap, uint64_t *d_totals,
+                                     void *stream);
 
 /* ------------------------------------------------------------------------ */
 /* Read feed: the local-storage read path (iterator/cursor.go:31-38 copies    */
@@ -482,12 +501,15 @@ typedef struct honu_feed_result {
     const uint64_t *rec_off;          /* n + 1 offsets into records */
     const honu_meta *meta;            /* n rows (NULL with HONU_FEED_HEADERS) */
     const honu_record_info *info;     /* n */
-    const honu_acl *acl;              /* acl_n entries */
+    const honu_acl *acl;              /* acl_n entries (never more than the table holds) */
     uint64_t acl_n;
-    const uint32_t *regions;          /* regions_n entries */
+    const uint32_t *regions;          /* regions_n entries (likewise) */
     uint64_t regions_n;
     const uint8_t *keys;              /* 29 * n bytes, Object.Key() (NULL with HEADERS) */
     const int32_t *key_status;        /* n */
+    uint64_t acl_needed;              /* entries the batch needed; > acl_n when the table
+                                         overflowed (those records: HONU_ERR_CAPACITY) */
+    uint64_t regions_needed;
 } honu_feed_result;
 
 /* A feed with two slots of batch_records records / batch_bytes bytes each.
@@ -611,6 +633,30 @@ int32_t honu_gen_payload(honu_ctx *ctx, uint64_t seed, uint64_t first, uint64_t 
  * [d_off[i], d_off[i]+d_len[i]) with d_off of length n. */
 int32_t honu_digest_records(honu_ctx *ctx, const uint8_t *d_arena, const uint64_t *d_off,
                             const uint64_t *d_len, uint64_t n, uint64_t *d_digest, void *stream);
+/* Round trip check of a decoded batch against the encode input it came from
+ * (bench and tests at full size, where the CPU oracle is too slow): record i
+ * was encoded from source row d_src[i] (spans into d_var, lists into d_src_acl
+ * / d_src_regions, payload length d_payload_off[i+1] - d_payload_off[i]) and
+ * decoded into d_dec[i] / d_info[i] (spans into the records arena d_rec,
+ * lists into d_dec_acl / d_dec_regions). d_mismatch[i] gets an OR of
+ * HONU_VERIFY_* bits, 0 when every row byte, span byte, ACL entry and region
+ * equals what the Go decoder returns for that input (nil structs zero,
+ * REGIONS_NONNIL set, nil ACL entries all-zero). Payload bytes are checked
+ * with honu_digest_records. */
+enum {
+    HONU_VERIFY_STATUS = 1u << 0,   /* a status is not OK, or len(Data()) differs */
+    HONU_VERIFY_PRESENT = 1u << 1,  /* presence bits */
+    HONU_VERIFY_FIELDS = 1u << 2,   /* a fixed row byte (scalars, ULIDs, span lengths, counts) */
+    HONU_VERIFY_SPANS = 1u << 3,    /* bytes of a MIME/schema/publisher/encryption span */
+    HONU_VERIFY_ACL = 1u << 4,      /* an ACL table entry */
+    HONU_VERIFY_REGIONS = 1u << 5   /* a region table entry */
+};
+int32_t honu_verify_decoded(honu_ctx *ctx, const honu_meta *d_src, const uint8_t *d_var,
+                            const honu_acl *d_src_acl, const uint32_t *d_src_regions,
+                            const uint64_t *d_payload_off, const uint8_t *d_rec,
+                            const honu_meta *d_dec, const honu_record_info *d_info,
+                            const honu_acl *d_dec_acl, const uint32_t *d_dec_regions, uint64_t n,
+                            uint32_t *d_mismatch, void *stream);
 /* The same digest of one host byte run. */
 uint64_t honu_digest_host(const uint8_t *p, uint64_t len);
 

@@ -988,21 +988,32 @@ static int decode_collection_body(oreader *r, uint64_t base, honu_collection *c,
     return HONU_OK;
 }
 
-int oracle_system_decode(const uint8_t *o, uint64_t len, uint64_t base, honu_collection *c,
-                         honu_acl *acl_out, uint64_t acl_cap, uint32_t *regions_out,
-                         uint64_t regions_cap, honu_index *idx_out, uint64_t idx_cap,
-                         uint64_t counts[3]) {
+/* headless = 0: object.UnmarshalSystem(obj, &Collection{}) (system.go:36-45);
+ * headless = 1: lani.Unmarshal(obj, &Collection{}) (lani.go:29-33), i.e.
+ * Collection.Decode from byte 0 of the raw value as store.go:367 calls it
+ * (the storage version byte and the struct flag are read as the ID). */
+static int collection_decode(const uint8_t *o, uint64_t len, uint64_t base, int headless,
+                             honu_collection *c, honu_acl *acl_out, uint64_t acl_cap,
+                             uint32_t *regions_out, uint64_t regions_cap, honu_index *idx_out,
+                             uint64_t idx_cap, uint64_t counts[3]) {
     memset(c, 0, sizeof *c);
     counts[0] = counts[1] = counts[2] = 0;
-    /* obj[1 : len(obj)-1] (system.go:40) panics for len < 2 */
-    if (len < 2) return HONU_ERR_PANIC;
-    oreader r = {o + 1, len - 2, 0};
     osyslists L = {acl_out, acl_cap, 0, regions_out, regions_cap, 0, idx_out, idx_cap, 0};
-    int present;
-    int st = r_bool(&r, &present);                   /* DecodeStruct(v) :41 */
-    if (st == HONU_OK && present) {
-        c->present = HONU_HAS_COLLECTION;
-        st = decode_collection_body(&r, base + 1, c, &L);
+    int st;
+    if (headless) {
+        oreader r = {o, len, 0};
+        c->present = HONU_HAS_COLLECTION;           /* the target itself, never nil */
+        st = decode_collection_body(&r, base, c, &L);
+    } else {
+        /* obj[1 : len(obj)-1] (system.go:40) panics for len < 2 */
+        if (len < 2) return HONU_ERR_PANIC;
+        oreader r = {o + 1, len - 2, 0};
+        int present;
+        st = r_bool(&r, &present);                   /* DecodeStruct(v) :41 */
+        if (st == HONU_OK && present) {
+            c->present = HONU_HAS_COLLECTION;
+            st = decode_collection_body(&r, base + 1, c, &L);
+        }
     }
     if (st != HONU_OK) {
         memset(c, 0, sizeof *c);
@@ -1012,6 +1023,14 @@ int oracle_system_decode(const uint8_t *o, uint64_t len, uint64_t base, honu_col
     counts[1] = L.reg_n;
     counts[2] = L.idx_n;
     return HONU_OK;
+}
+
+int oracle_system_decode(const uint8_t *o, uint64_t len, uint64_t base, honu_collection *c,
+                         honu_acl *acl_out, uint64_t acl_cap, uint32_t *regions_out,
+                         uint64_t regions_cap, honu_index *idx_out, uint64_t idx_cap,
+                         uint64_t counts[3]) {
+    return collection_decode(o, len, base, 0, c, acl_out, acl_cap, regions_out, regions_cap,
+                             idx_out, idx_cap, counts);
 }
 
 int oracle_system_marshal_batch(const honu_collection *rows, const uint8_t *var, uint64_t var_len,
@@ -1046,10 +1065,11 @@ int oracle_system_marshal_batch(const honu_collection *rows, const uint8_t *var,
     return any_cap ? HONU_ERR_CAPACITY : HONU_OK;
 }
 
-int oracle_system_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
-                               honu_collection *rows, int32_t *status, honu_acl *acl,
-                               uint64_t acl_cap, uint32_t *regions, uint64_t regions_cap,
-                               honu_index *idx, uint64_t idx_cap, uint64_t totals[3]) {
+static int collection_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                                   int headless, honu_collection *rows, int32_t *status,
+                                   honu_acl *acl, uint64_t acl_cap, uint32_t *regions,
+                                   uint64_t regions_cap, honu_index *idx, uint64_t idx_cap,
+                                   uint64_t totals[3]) {
     uint64_t pos[3] = {0, 0, 0};
     int any_cap = 0;
     for (uint64_t i = 0; i < n; i++) {
@@ -1061,7 +1081,8 @@ int oracle_system_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint
         uint64_t ac = acl && pos[0] < acl_cap ? acl_cap - pos[0] : 0;
         uint64_t rc = regions && pos[1] < regions_cap ? regions_cap - pos[1] : 0;
         uint64_t xc = idx && pos[2] < idx_cap ? idx_cap - pos[2] : 0;
-        int st = oracle_system_decode(rec + beg, len, beg, &rows[i], ao, ac, ro, rc, xo, xc, cnt);
+        int st = collection_decode(rec + beg, len, beg, headless, &rows[i], ao, ac, ro, rc, xo, xc,
+                                   cnt);
         if (st == HONU_OK) {
             if (rows[i].acl_count) rows[i].acl_off = pos[0];
             if (rows[i].regions_count) rows[i].regions_off = pos[1];
@@ -1078,4 +1099,20 @@ int oracle_system_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint
     if (totals)
         for (int k = 0; k < 3; k++) totals[k] = pos[k];
     return any_cap ? HONU_ERR_CAPACITY : HONU_OK;
+}
+
+int oracle_system_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                               honu_collection *rows, int32_t *status, honu_acl *acl,
+                               uint64_t acl_cap, uint32_t *regions, uint64_t regions_cap,
+                               honu_index *idx, uint64_t idx_cap, uint64_t totals[3]) {
+    return collection_decode_batch(rec, rec_off, n, 0, rows, status, acl, acl_cap, regions,
+                                   regions_cap, idx, idx_cap, totals);
+}
+
+int oracle_collection_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                                   honu_collection *rows, int32_t *status, honu_acl *acl,
+                                   uint64_t acl_cap, uint32_t *regions, uint64_t regions_cap,
+                                   honu_index *idx, uint64_t idx_cap, uint64_t totals[3]) {
+    return collection_decode_batch(rec, rec_off, n, 1, rows, status, acl, acl_cap, regions,
+                                   regions_cap, idx, idx_cap, totals);
 }

@@ -110,6 +110,13 @@ int oracle_system_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint
                                honu_collection *rows, int32_t *status, honu_acl *acl,
                                uint64_t acl_cap, uint32_t *regions, uint64_t regions_cap,
                                honu_index *idx, uint64_t idx_cap, uint64_t totals[3]);
+/* lani.Unmarshal(raw, &metadata.Collection{}) (lani.go:29-33) per record:
+ * Collection.Decode (collection.go:240-356) from byte 0 of the raw value, as
+ * store.go:367 calls it on a bbolt value that holds a whole system object. */
+int oracle_collection_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                                   honu_collection *rows, int32_t *status, honu_acl *acl,
+                                   uint64_t acl_cap, uint32_t *regions, uint64_t regions_cap,
+                                   honu_index *idx, uint64_t idx_cap, uint64_t totals[3]);
 
 #ifdef __cplusplus
 }

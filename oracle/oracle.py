@@ -12,7 +12,9 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhonu_oracle.so")
+# HONU_ORACLE_LIB: an alternative build of the same oracle (the ASan/UBSan
+# one, oracle/Makefile `sanitize`)
+LIB_PATH = os.environ.get("HONU_ORACLE_LIB") or os.path.join(_HERE, "libhonu_oracle.so")
 _lib = None
 P, U64, I32 = C.c_void_p, C.c_uint64, C.c_int32
 
@@ -45,6 +47,7 @@ def load():
         "oracle_system_marshal_batch": (C.c_int, [P, P, U64, P, U64, P, U64, P, U64, U64, P, U64,
                                                   P, P]),
         "oracle_system_decode_batch": (C.c_int, [P, P, U64, P, P, P, U64, P, U64, P, U64, P]),
+        "oracle_collection_decode_batch": (C.c_int, [P, P, U64, P, P, P, U64, P, U64, P, U64, P]),
     }
     for name, (res, args) in protos.items():
         fn = getattr(lib, name)
@@ -149,8 +152,9 @@ def system_marshal_batch(sb):
     return out[:total], out_off, status
 
 
-def system_decode_batch(rec: np.ndarray, rec_off: np.ndarray):
-    """UnmarshalSystem(obj, &Collection{}) -> (rows, status, acl, regions, index, totals)."""
+def system_decode_batch(rec: np.ndarray, rec_off: np.ndarray, headless: bool = False):
+    """UnmarshalSystem(obj, &Collection{}) -> (rows, status, acl, regions, index, totals);
+    headless: lani.Unmarshal(obj, &Collection{}) instead (store.go:367)."""
     from honu_amd.metadata import ACL_DTYPE
     from honu_amd.system import COLLECTION_DTYPE, INDEX_DTYPE
     lib = load()
@@ -166,8 +170,9 @@ def system_decode_batch(rec: np.ndarray, rec_off: np.ndarray):
     reg = np.zeros(nbytes + 1, np.uint32)
     idx = np.zeros(nbytes + 1, INDEX_DTYPE)
     totals = np.zeros(3, np.uint64)
-    lib.oracle_system_decode_batch(_p(rec), _p(rec_off), n, _p(rows), _p(status), _p(acl),
-                                   len(acl), _p(reg), len(reg), _p(idx), len(idx), _p(totals))
+    fn = lib.oracle_collection_decode_batch if headless else lib.oracle_system_decode_batch
+    fn(_p(rec), _p(rec_off), n, _p(rows), _p(status), _p(acl), len(acl), _p(reg), len(reg),
+       _p(idx), len(idx), _p(totals))
     return (rows[:n], status[:n], acl[: int(totals[0])], reg[: int(totals[1])],
             idx[: int(totals[2])], totals)
 

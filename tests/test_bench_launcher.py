@@ -1,0 +1,50 @@
+"""bench.py --gpus N launches its own ranks (the driver's scaling runs call it
+without torchrun) and refuses to run on fewer GPUs than asked for."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(kw)
+    return env
+
+
+def _run(args, env=None, timeout=240):
+    return subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True,
+                          env=env or _env(), timeout=timeout)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_launcher_spawns_ranks(world):
+    r = _run(["--gpus", str(world), "--dry-run", "--records", "1000"])
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # only rank 0 prints
+    out = json.loads(lines[0])
+    assert out["dry_run"] and out["ranks"] == world
+    shards = sorted(out["shards"])
+    assert [s[0] for s in shards] == list(range(world))          # distinct RANKs
+    assert len({s[3] for s in shards}) == world                   # distinct processes
+    assert [(s[1], s[2]) for s in shards] == [(1000 * r, 1000) for r in range(world)]  # disjoint
+
+
+def test_launcher_refuses_missing_gpus():
+    import torch
+    want = max(2, torch.cuda.device_count() + 1)
+    r = _run(["--gpus", str(want), "--records", "10"])
+    assert r.returncode != 0
+    assert f"needs {want} GPUs" in r.stderr
+
+
+def test_world_size_must_match():
+    r = _run(["--gpus", "1", "--records", "10"], env=_env(WORLD_SIZE="2", RANK="0"))
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr

@@ -1,0 +1,140 @@
+"""The bench's exact timed pipeline against the CPU oracle, byte for byte.
+
+bench.py times a pipelined form of the codec that no other test drives: per
+chunk, the size pass + scan, the header/tail encoder and the decode parse /
+tables run on one stream while the payload copies run on a second stream, the
+encode copy starting after the scan so it writes payload bytes into the same
+16-byte chunks the header/tail encoder is writing around them; two output
+slots alternate across chunks and across steps. Here Bench itself runs that
+pipeline on small batches split into 5 chunks for 2 steps, and every chunk of
+every step is compared with oracle.marshal_batch / oracle.decode_batch once it
+has drained (while the next chunk runs): encoded bytes, offsets, statuses,
+full 352-byte rows, record info, ACL and region tables and every materialised
+payload."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+import bench  # noqa: E402
+from honu_amd import _lib  # noqa: E402
+from honu_amd.metadata import HostBatch  # noqa: E402
+from honu_amd.workload import gen_host_batch  # noqa: E402
+
+
+def _host(t, nbytes, dtype=np.uint8):
+    return t[:nbytes].cpu().numpy().view(dtype)
+
+
+@pytest.fixture(autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.mark.parametrize("after", ["scan", "meta"])
+@pytest.mark.parametrize("shape,n", [("small", 4000), ("mixed", 1200), ("large", 160)])
+def test_bench_pipeline_bit_exact(oracle_lib, shape, n, after):
+    seed = 7
+    args = bench.parse_args(["--records", str(n), "--shape", shape, "--min-chunks", "5",
+                             "--encode-copy-after", after, "--seed", str(seed)])
+    b = bench.Bench(args, 0, 0)
+    assert len(b.chunks) >= 5 and len(b.slots) == 2
+    hb = gen_host_batch(seed, shape, 0, n)  # the same records the device generator made
+    seen = []
+
+    def check(a, z, sl):
+        m = z - a
+        sub = HostBatch(hb.meta[a:z], hb.var, hb.acl, hb.regions, hb.payload,
+                        hb.payload_off[a:z + 1])
+        oout, ooff, ost = oracle_lib.marshal_batch(sub)
+        assert (ost == 0).all()
+        assert np.array_equal(_host(sl.status, 4 * m, np.int32), ost)
+        assert np.array_equal(_host(sl.out_off, 8 * (m + 1), np.uint64), ooff)
+        assert _host(sl.out, int(ooff[-1])).tobytes() == oout.tobytes(), (a, z)
+        ometa, oinfo, oacl, oreg, odata, otot = oracle_lib.decode_batch(oout, ooff, True)
+        assert np.array_equal(_host(sl.totals, 24, np.uint64), otot)
+        assert _host(sl.dmeta, 352 * m).tobytes() == ometa.tobytes()
+        assert _host(sl.dinfo, 32 * m).tobytes() == oinfo.tobytes()
+        assert _host(sl.dacl, 20 * int(otot[0])).tobytes() == oacl.tobytes()
+        assert _host(sl.dreg, 4 * int(otot[1])).tobytes() == oreg.tobytes()
+        data = _host(sl.data, int(otot[2]))
+        for i in range(m):
+            o, ln = int(oinfo[i]["data_off"]), int(oinfo[i]["data_len"])
+            assert data[o:o + ln].tobytes() == odata[o:o + ln].tobytes(), (a + i)
+        # the bench's own device-side check agrees
+        assert b._verify_chunk(a, z, sl)
+        seen.append((a, z, sl))
+        return True
+
+    for _ in range(2):
+        assert b.step(check=check)
+    torch.cuda.synchronize()
+    assert [x[:2] for x in seen] == b.chunks * 2
+    # slots alternate across chunks and across steps (5 chunks: step 2 starts on slot 1)
+    slots = [id(x[2]) for x in seen]
+    assert all(p != q for p, q in zip(slots, slots[1:]))
+
+
+def test_bench_verify_detects_corruption():
+    """_verify_chunk (honu_verify_decoded + digests) flags one wrong byte in a
+    decoded ObjectID, span, ACL entry, region or payload."""
+    args = bench.parse_args(["--records", "600", "--shape", "small", "--min-chunks", "1"])
+    b = bench.Bench(args, 0, 0)
+    (a, z), = b.chunks
+    sl = b._issue(a, z, False)
+    torch.cuda.synchronize()
+    assert b._verify_chunk(a, z, sl)
+    m = z - a
+    rows = _host(sl.dmeta, 352 * m, np.uint8).copy().reshape(m, 352)
+    tot = _host(sl.totals, 24, np.uint64)
+
+    def flip(t, k):
+        v = t[k:k + 1].clone()
+        t[k:k + 1] = v ^ 0x5A
+        torch.cuda.synchronize()
+        ok = b._verify_chunk(a, z, sl)
+        t[k:k + 1] = v
+        torch.cuda.synchronize()
+        return ok
+
+    i = 17
+    mime = int(rows[i, 208:216].view(np.uint64)[0])
+    assert not flip(sl.dmeta, 352 * i + 96)          # ObjectID byte
+    assert not flip(sl.dmeta, 352 * i + 11)          # padding must stay zero
+    assert not flip(sl.out, mime)                    # a MIME span byte in the records arena
+    assert not flip(sl.dacl, 20 * (int(tot[0]) // 2) + 3)
+    assert not flip(sl.dreg, 4 * (int(tot[1]) // 2))
+    info = _host(sl.dinfo, 32 * m, np.uint64).reshape(m, 4)
+    assert not flip(sl.data, int(info[i, 0]) + 5)    # a payload byte
+    assert b._verify_chunk(a, z, sl)
+
+
+def test_encode_payloads_respects_out_cap(oracle_lib):
+    """honu_encode_payloads run without the header/tail encoder's capacity
+    verdict (another stream) writes nothing past out_cap."""
+    from honu_amd import object as hobj
+    hb = gen_host_batch(3, "small", 0, 200)
+    oout, ooff, _ = oracle_lib.marshal_batch(hb)
+    codec = hobj.Codec(0, 1024)
+    d = hobj.DeviceBatch.from_host(hb, codec.torch_device)
+    total = int(ooff[-1])
+    cap = int(ooff[120]) + 7  # record 120 does not fit
+    out = torch.full((total + 4096,), 0xEE, dtype=torch.uint8, device=codec.torch_device)
+    off = torch.from_numpy(ooff.view(np.uint8).copy()).to(codec.torch_device)
+    st = torch.zeros(4 * 200, dtype=torch.uint8, device=codec.torch_device)  # size pass: all OK
+    _lib.check(codec.lib.honu_encode_payloads(codec.ctx, _lib.ptr(d.payload),
+                                              _lib.ptr(d.payload_off), 200, _lib.ptr(out), cap,
+                                              _lib.ptr(off), _lib.ptr(st), codec.stream), "copy")
+    torch.cuda.synchronize()
+    h = out.cpu().numpy()
+    assert (h[cap:] == 0xEE).all()
+    # the records that fit got their payload bytes
+    for i in (0, 50, 119):
+        s = int(ooff[i])
+        plen = int(hb.payload_off[i + 1] - hb.payload_off[i])
+        hl = 1 + len(oracle_lib.put_uvarint(plen))
+        assert h[s + hl:s + hl + plen].tobytes() == oout[s + hl:s + hl + plen].tobytes()
+    codec.close()

@@ -37,7 +37,7 @@ def _raw_copy(v):
 
 def _copy(res):
     """Results are views of pinned buffers reused by the next fill: copy."""
-    return {k: (None if v is None else _raw_copy(v)) for k, v in vars(res).items()}
+    return {k: (_raw_copy(v) if isinstance(v, np.ndarray) else v) for k, v in vars(res).items()}
 
 
 def _drive(feed, objs):
@@ -233,4 +233,35 @@ def test_feed_append_batch(oracle_lib):
         meta, info, *_ = oracle_lib.decode_batch(r["records"], r["rec_off"])
         assert r["info"].tobytes() == info.tobytes() and r["meta"].tobytes() == meta.tobytes()
         first += got
+    feed.close()
+
+
+@pytest.mark.gpu
+def test_feed_acl_table_overflow(oracle_lib):
+    """A nil-entry flood (1 byte per ACL entry) needs more table entries than
+    the feed holds (batch_bytes/8 + 1024): the flooded record gets
+    HONU_ERR_CAPACITY, acl_n never exceeds the table and acl_needed reports
+    what the batch needed; the records before it decode as the oracle says."""
+    from honu_amd.feed import RecordFeed
+    from honu_amd.metadata import Metadata, pack_batch
+    flood = Metadata(ACL=[None] * 60000)
+    hb = gen_host_batch(5, "small", 0, 4)
+    rec, off, _ = oracle_lib.marshal_batch(hb)
+    objs = [rec[int(off[i]):int(off[i + 1])].tobytes() for i in range(4)]
+    frec, foff, fst = oracle_lib.marshal_batch(pack_batch([flood], [b"x" * 10]))
+    assert fst[0] == 0
+    objs.append(frec.tobytes())
+    feed = RecordFeed(0, 64, 1 << 17)
+    for o in objs:
+        assert feed.append(o) == 0
+    res = feed.wait(feed.submit())
+    cap = (1 << 17) // 8 + 1024
+    good = sum(int(hb.meta[i]["acl_count"]) for i in range(4))
+    assert res.acl_needed == good + 60000
+    assert len(res.acl) == min(res.acl_needed, cap) <= cap
+    assert res.info["meta_status"][4] == 9  # HONU_ERR_CAPACITY
+    assert (res.info["meta_status"][:4] == 0).all()
+    ometa, oinfo, oacl, oreg, _, _ = oracle_lib.decode_batch(rec, off)
+    assert res.acl[:good].tobytes() == oacl.tobytes()
+    assert res.meta[:4].tobytes() == ometa.tobytes()
     feed.close()

@@ -136,6 +136,41 @@ def test_decode_error_vectors(oracle_lib):
     assert not rows["present"].any()
 
 
+def test_headless_collection_decode(oracle_lib):
+    """lani.Unmarshal(raw, &Collection{}) as store.go:367 calls it on a raw
+    bbolt value (Collection.Decode from byte 0, collection.go:240-356):
+    lani.Marshal(c)'s bytes -- the system object without its version byte,
+    struct flag and trailing nil-metadata flag (system.go:17-28) -- decode to
+    c; a whole system object is decoded with its first two bytes read as the
+    start of the ID; short values give the DecodeULID errors
+    (decode.go:209-221)."""
+    cols = random_batch(11, 120, big_every=30)
+    cols = [c for c in cols if c is not None] + [
+        collection_from_json(load_json("object_collection.json"))]
+    out, off, st = oracle_lib.system_marshal_batch(pack_system_batch(cols))
+    bodies = [out[int(off[i]) + 2:int(off[i + 1]) - 1].tobytes() for i in range(len(cols))]
+    boff = np.zeros(len(bodies) + 1, np.uint64)
+    boff[1:] = np.cumsum([len(b) for b in bodies])
+    brec = np.frombuffer(b"".join(bodies), np.uint8)
+    rows, st, acl, reg, idx, _ = oracle_lib.system_decode_batch(brec, boff, headless=True)
+    assert (st == 0).all()
+    for i, c in enumerate(cols):
+        assert unpack_collection(rows[i], brec, acl, reg, idx) == normalize_collection(c), i
+    raw = out[int(off[-2]):int(off[-1])].tobytes()  # the fixture's system object, as stored
+    cases = [b"", b"\x01\x00\x00", bytes(15), raw]
+    coff = np.zeros(len(cases) + 1, np.uint64)
+    coff[1:] = np.cumsum([len(b) for b in cases])
+    crec = np.frombuffer(b"".join(cases), np.uint8)
+    rows, st, *_ = oracle_lib.system_decode_batch(crec, coff, headless=True)
+    assert st[:3].tolist() == [3, 4, 4]  # io.EOF, io.ErrUnexpectedEOF x2
+    # the stored fixture: ID = raw[0:16] (01 01 + the real ID's first 14
+    # bytes); the Name length is the uvarint of the real ID's last two bytes
+    # (8c 4a -> 9484), longer than what is left: io.ErrUnexpectedEOF
+    # (decode.go:46-48)
+    assert raw[:2] == b"\x01\x01" and raw[16:18] == b"\x8c\x4a"
+    assert st[3] == 4
+
+
 # --------------------------------------------------------------------------
 # GPU vs oracle
 # --------------------------------------------------------------------------
@@ -196,6 +231,31 @@ def test_gpu_system_decode_parity(oracle_lib):
 
 
 @pytest.mark.gpu
+def test_gpu_headless_collection_decode_parity(oracle_lib):
+    """honu_collection_decode_batch (lani.Unmarshal(raw, &Collection{}),
+    store.go:367) against the oracle on whole system objects, their
+    lani.Marshal bodies and the malformed corpus."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from honu_amd.system import decode_system_batch
+    objs = _corpus(oracle_lib, seed=6)
+    objs += [o[2:-1] for o in objs[:64] if len(o) > 3]
+    off = np.zeros(len(objs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(o) for o in objs])
+    rec = np.frombuffer(b"".join(objs) + b"\0", np.uint8)[: int(off[-1])]
+    rows, st, acl, reg, idx, tot = decode_system_batch(rec, off, headless=True)
+    orows, ost, oacl, oreg, oidx, otot = oracle_lib.system_decode_batch(rec, off, headless=True)
+    assert np.array_equal(tot, otot)
+    assert st.tolist() == ost.tolist()
+    assert rows.tobytes() == orows.tobytes()
+    assert acl.tobytes() == oacl.tobytes()
+    assert reg.tobytes() == oreg.tobytes()
+    assert idx.tobytes() == oidx.tobytes()
+    assert 0 in set(st.tolist()) and len(set(st.tolist())) >= 4
+
+
+@pytest.mark.gpu
 def test_gpu_marshal_unmarshal_system_api():
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
@@ -212,3 +272,9 @@ def test_gpu_marshal_unmarshal_system_api():
         UnmarshalSystem(b"\x01")
     with pytest.raises(hobj.EOFError_):
         UnmarshalSystem(b"\x01\x00")
+    from honu_amd.system import Unmarshal
+    assert Unmarshal(obj[2:-1], Collection()) == normalize_collection(c)
+    with pytest.raises(hobj.GoPanic):  # store.go:155: a nil *Collection
+        Unmarshal(obj, None)
+    with pytest.raises(hobj.ErrUnexpectedEOF):
+        Unmarshal(b"\x01\x00\x00", Collection())

@@ -70,7 +70,7 @@ def main():
                 "scan": lambda: L.honu_exclusive_scan(c, P(out_off), n, P(out_off), s),
                 "encode_meta": lambda: L.honu_encode_records(c, P(dm), P(dv), P(da), P(dr), P(do), n,
                                                              P(out), cap, P(out_off), P(st), s),
-                "encode_copy": lambda: L.honu_encode_payloads(c, P(pay), P(do), n, P(out),
+                "encode_copy": lambda: L.honu_encode_payloads(c, P(pay), P(do), n, P(out), cap,
                                                               P(out_off), P(st), s),
                 "parse": lambda: L.honu_decode_parse(c, P(out), P(out_off), n, P(dmeta), P(dinfo), s),
                 "tables": lambda: L.honu_decode_tables(c, P(out), n, P(dmeta), P(dinfo), P(dacl),

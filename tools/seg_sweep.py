@@ -44,10 +44,10 @@ def main():
         ooff = torch.arange(n + 1, dtype=torch.int64, device=dev) * (sz + a.gap)
         st = torch.zeros(n, dtype=torch.int32, device=dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        _lib.check(L.honu_encode_payloads(c, P(pay), P(poff), n, P(out), P(ooff), P(st), s), "copy")
+        _lib.check(L.honu_encode_payloads(c, P(pay), P(poff), n, P(out), out.numel(), P(ooff), P(st), s), "copy")
         e0.record()
         for _ in range(a.reps):
-            _lib.check(L.honu_encode_payloads(c, P(pay), P(poff), n, P(out), P(ooff), P(st), s), "copy")
+            _lib.check(L.honu_encode_payloads(c, P(pay), P(poff), n, P(out), out.numel(), P(ooff), P(st), s), "copy")
         e1.record()
         torch.cuda.synchronize()
         t = e0.elapsed_time(e1) / 1e3 / a.reps

@@ -70,7 +70,7 @@ def main():
             _lib.check(L.honu_ctx_set_param(c, b"copy_blocks", b * ncu), "p")
             _lib.check(L.honu_ctx_set_param(c, b"copy_variant", v), "p")
             for k, fn in enumerate((
-                lambda: L.honu_encode_payloads(c, P(pay), P(do), n, P(out), P(out_off), P(st), s),
+                lambda: L.honu_encode_payloads(c, P(pay), P(do), n, P(out), out.numel(), P(out_off), P(st), s),
                 lambda: L.honu_decode_payloads(c, P(out), n, P(dinfo), P(data), P(tot), s))):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
