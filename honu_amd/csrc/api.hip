@@ -24,6 +24,11 @@ struct honu_ctx {
     DecodeScratch *scratch;  // max_n
     uint32_t *reg_inline;    // 8 * max_n: region ids handed from the group parse to fill
     uint64_t *enc_acl;       // max_n: ACL list positions, lane encoder -> group ACL encoder
+    // decoupled look-back state of the fused kernels (fused.hip): per kernel
+    // a ticket/epoch block and K status words per 64-record tile
+    LbState *lb_dec, *lb_enc;
+    uint64_t *lb_dec_status, *lb_enc_status;
+    uint64_t lb_dec_words, lb_enc_words;
 };
 
 static thread_local char g_last_error[256];
@@ -44,6 +49,17 @@ static int32_t arg_fail(const char *what) {
 }
 
 static bool aligned(const void *p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
+
+// record_variant 5 runs the batch entries through the split kernels of
+// variant 0 (the fused kernels are variant 0's batch path)
+static int split_rv(int rv) { return rv == 5 ? 0 : rv; }
+
+// Fused kernels: persistent waves (2 workgroups of 4 waves per CU fit the LDS
+// and registers), fewer under a lane_blocks cap.
+static int fused_blocks(const LaunchGeom &g) {
+    const int resident = 2 * g.num_cu;
+    return g.lane_blocks > 0 && g.lane_blocks < resident ? g.lane_blocks : resident;
+}
 
 static int env_int(const char *name, int dflt) {
     const char *v = getenv(name);
@@ -116,8 +132,10 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     const uint64_t n = c->max_n;
     const uint64_t np = scan_partials_len(n, 3) + scan_partials_len(n, 1);
     const uint64_t map_cap = 1ull << 22;  // tile map entries (sweep copy variants)
-    const uint64_t bytes =
-        8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 32 * n + 8 * n + 4 * map_cap + 256;
+    const uint64_t tiles = (n + HONU_WAVE - 1) / HONU_WAVE;
+    const uint64_t lb_bytes = 2 * sizeof(LbState) + 8 * (3 * tiles + 1 * tiles);
+    const uint64_t bytes = 8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 32 * n +
+                           8 * n + 4 * map_cap + lb_bytes + 256;
     if (hipMalloc(&c->ws, bytes) != hipSuccess) {
         snprintf(g_last_error, sizeof g_last_error, "hipMalloc(%llu) failed",
                  (unsigned long long)bytes);
@@ -139,6 +157,19 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->enc_acl = (uint64_t *)(c->reg_inline + 8 * n);
     c->geom.tile_map = (uint32_t *)(c->enc_acl + n);
     c->geom.tile_map_cap = map_cap;
+    c->lb_dec = (LbState *)(c->geom.tile_map + map_cap);
+    c->lb_enc = c->lb_dec + 1;
+    c->lb_dec_status = (uint64_t *)(c->lb_enc + 1);
+    c->lb_dec_words = 3 * tiles;
+    c->lb_enc_status = c->lb_dec_status + c->lb_dec_words;
+    c->lb_enc_words = tiles;
+    // clean look-back state: epoch 0 with no published tile
+    if (hipMemset(c->lb_dec, 0, lb_bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(c->ws);
+        free(c);
+        *err = HONU_E_HIP;
+        return nullptr;
+    }
     return c;
 }
 
@@ -173,7 +204,7 @@ int32_t honu_encode_sizes(honu_ctx *ctx, const honu_meta *d_meta, uint64_t var_l
     if (n && (!d_meta || !d_payload_off || !d_sizes)) return arg_fail("null pointer");
     if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
     HIPCHK(hipSetDevice(ctx->device));
-    const int rv = ctx->geom.record_variant;
+    const int rv = split_rv(ctx->geom.record_variant);
     if (rv == 0 || rv == 2 || rv == 4)
         HIPCHK(launch_encode_sizes_grp(d_meta, var_len, d_acl, acl_len, d_regions, regions_len,
                                        d_payload_off, n, d_sizes, d_status, ctx->geom.lane_blocks,
@@ -208,7 +239,7 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
         return arg_fail("null pointer");
     if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
     HIPCHK(hipSetDevice(ctx->device));
-    const int rv = ctx->geom.record_variant;
+    const int rv = split_rv(ctx->geom.record_variant);
     if (rv == 2)
         HIPCHK(launch_encode_meta_grp(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
                                       out_cap, d_out_off, d_status, ctx->geom.lane_blocks,
@@ -256,12 +287,44 @@ int32_t honu_encode(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var
                                 d_status, stream);
 }
 
+int32_t honu_marshal_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
+                             uint64_t var_len, const honu_acl *d_acl, uint64_t acl_len,
+                             const uint32_t *d_regions, uint64_t regions_len,
+                             const uint64_t *d_payload_off, uint64_t n, uint8_t *d_out,
+                             uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status,
+                             void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n > ctx->max_n) return HONU_E_WORKSPACE;
+    if (!d_out_off) return arg_fail("null pointer");
+    if (n && (!d_meta || !d_payload_off || !d_status)) return arg_fail("null pointer");
+    if (!aligned(d_meta, 16)) return arg_fail("rows must be 16-byte aligned");
+    if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        HIPCHK(hipMemsetAsync(d_out_off, 0, sizeof(uint64_t), s));
+        return HONU_OK;
+    }
+    HIPCHK(launch_encode_fused(d_meta, d_var, var_len, d_acl, acl_len, d_regions, regions_len,
+                               d_payload_off, n, d_out, out_cap, d_out_off, d_status, ctx->lb_enc,
+                               ctx->lb_enc_status, ctx->lb_enc_words, fused_blocks(ctx->geom), s));
+    return HONU_OK;
+}
+
 int32_t honu_marshal_batch(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
                            uint64_t var_len, const honu_acl *d_acl, uint64_t acl_len,
                            const uint32_t *d_regions, uint64_t regions_len,
                            const uint8_t *d_payload, const uint64_t *d_payload_off, uint64_t n,
                            uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off,
                            int32_t *d_status, void *stream) {
+    if (ctx && ctx->geom.record_variant == 0) {  // fused (default)
+        int32_t st = honu_marshal_records(ctx, d_meta, d_var, var_len, d_acl, acl_len, d_regions,
+                                          regions_len, d_payload_off, n, d_out, out_cap, d_out_off,
+                                          d_status, stream);
+        if (st) return st;
+        return honu_encode_payloads(ctx, d_payload, d_payload_off, n, d_out, out_cap, d_out_off,
+                                    d_status, stream);
+    }
     int32_t st = honu_encode_sizes(ctx, d_meta, var_len, d_acl, acl_len, d_regions, regions_len,
                                    d_payload_off, n, d_out_off, d_status, stream);
     if (st) return st;
@@ -282,7 +345,7 @@ int32_t honu_decode_parse(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
     if (!aligned(d_rec, 16) || !aligned(d_meta, 16) || !aligned(d_info, 8))
         return arg_fail("records arena and rows must be 16-byte aligned");
     HIPCHK(hipSetDevice(ctx->device));
-    const int rv = ctx->geom.record_variant;
+    const int rv = split_rv(ctx->geom.record_variant);
     if (rv == 2)
         HIPCHK(launch_decode_parse_grp(d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
                                        ctx->reg_inline, ctx->counts, ctx->geom.lane_blocks,
@@ -315,7 +378,7 @@ int32_t honu_decode_tables(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n, honu
     hipStream_t s = (hipStream_t)stream;
     uint64_t *tot = d_totals ? d_totals : ctx->totals;
     HIPCHK(launch_scan(ctx->counts, n, 3, ctx->offs, tot, ctx->partials, s));
-    const int rv = ctx->geom.record_variant;
+    const int rv = split_rv(ctx->geom.record_variant);
     if (rv == 0 || rv == 2 || rv == 4)
         HIPCHK(launch_decode_fill_grp(d_rec, n, d_meta, d_info, ctx->scratch, ctx->reg_inline,
                                       ctx->counts, ctx->offs, d_acl, acl_cap, d_regions,
@@ -356,11 +419,46 @@ int32_t honu_decode_fill(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_
     return honu_decode_payloads(ctx, d_rec, n, d_info, d_data, d_totals, stream);
 }
 
+int32_t honu_decode_records(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
+                            uint64_t n, honu_meta *d_meta, honu_record_info *d_info,
+                            honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
+                            uint64_t regions_cap, int32_t materialize, uint64_t data_cap,
+                            uint64_t *d_totals, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n > ctx->max_n) return HONU_E_WORKSPACE;
+    if (n && (!d_rec || !d_rec_off || !d_meta || !d_info)) return arg_fail("null pointer");
+    if (!aligned(d_rec, 16) || !aligned(d_meta, 16) || !aligned(d_info, 8))
+        return arg_fail("records arena and rows must be 16-byte aligned");
+    if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
+    if (acl_cap && !d_acl) return arg_fail("acl table");
+    if (regions_cap && !d_regions) return arg_fail("region table");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    uint64_t *tot = d_totals ? d_totals : ctx->totals;
+    if (n == 0) {
+        HIPCHK(hipMemsetAsync(tot, 0, 3 * sizeof(uint64_t), s));
+        return HONU_OK;
+    }
+    HIPCHK(launch_decode_fused(d_rec, d_rec_off, n, d_meta, d_info, d_acl, acl_cap, d_regions,
+                               regions_cap, materialize != 0, data_cap, ctx->scratch, ctx->offs,
+                               tot, ctx->lb_dec, ctx->lb_dec_status, ctx->lb_dec_words,
+                               fused_blocks(ctx->geom), s));
+    return HONU_OK;
+}
+
 int32_t honu_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
                           uint64_t n, honu_meta *d_meta, honu_record_info *d_info,
                           honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
                           uint64_t regions_cap, uint8_t *d_data, uint64_t data_cap,
                           uint64_t *d_totals, void *stream) {
+    if (ctx && ctx->geom.record_variant == 0) {  // fused (default)
+        if (d_data && !aligned(d_data, 16)) return arg_fail("data arena must be 16-byte aligned");
+        int32_t st = honu_decode_records(ctx, d_rec, d_rec_off, n, d_meta, d_info, d_acl, acl_cap,
+                                         d_regions, regions_cap, d_data != nullptr, data_cap,
+                                         d_totals, stream);
+        if (st || !d_data) return st;
+        return honu_decode_payloads(ctx, d_rec, n, d_info, d_data, d_totals, stream);
+    }
     int32_t st = honu_decode_parse(ctx, d_rec, d_rec_off, n, d_meta, d_info, stream);
     if (st) return st;
     return honu_decode_fill(ctx, d_rec, d_rec_off, n, d_meta, d_info, d_acl, acl_cap, d_regions,

@@ -105,6 +105,9 @@ template <typename P> HONU_DEV uint32_t put_uvarint(P p, uint64_t x) {
 // byte-stream copy engine
 // ------------------------------------------------------------------------
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// 16 bytes at any byte address: one global_load_dwordx4 (gfx950 runs with
+// unaligned global access enabled)
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
 
 // Funnel a 16-byte output chunk out of two aligned 16-byte source chunks: the
 // bytes [p, p+16) of lo||hi, p in [0,16). p is wave-uniform, so the switch is
@@ -165,7 +168,8 @@ HONU_DEV void wave_copy_bytes(uint8_t *__restrict__ dst, const uint8_t *__restri
 // aligned 16-byte block holding at least one source byte never crosses a
 // page, so the over-read is always mapped.
 // NT: non-temporal cache policy, 0 none, 1 loads and stores, 2 loads only,
-// 3 stores only
+// 3 stores only; 4: a misaligned source is read with one unaligned 16-byte
+// load per chunk instead of two aligned loads and a funnel
 template <int UNROLL = 4, int NT = 0>
 HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint64_t n) {
     if (n == 0) return;
@@ -194,6 +198,17 @@ HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ s
 #pragma unroll
             for (int u = 0; u < UNROLL; u++)
                 if (c + u * HONU_WAVE < chunks) st16<(NT == 1 || NT == 3)>(&d4[c + u * HONU_WAVE], v[u]);
+        }
+    } else if (NT == 4) {
+        for (uint64_t c = lane; c < chunks; c += UNROLL * HONU_WAVE) {
+            u32x4 v[UNROLL];
+#pragma unroll
+            for (int u = 0; u < UNROLL; u++)
+                if (c + u * HONU_WAVE < chunks)
+                    v[u] = *reinterpret_cast<const u32x4u *>(src + 16 * (c + u * HONU_WAVE));
+#pragma unroll
+            for (int u = 0; u < UNROLL; u++)
+                if (c + u * HONU_WAVE < chunks) d4[c + u * HONU_WAVE] = v[u];
         }
     } else {
         const u32x4 *__restrict__ s4 = reinterpret_cast<const u32x4 *>(src - p);

@@ -212,6 +212,9 @@ static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
     case 5: hipLaunchKernelGGL((k_copy_segments<Seg, 16, 0>), grid, block, 0, s, seg, n, total); break;
     case 11: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 2>), grid, block, 0, s, seg, n, total); break;
     case 12: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 3>), grid, block, 0, s, seg, n, total); break;
+    case 13: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 4>), grid, block, 0, s, seg, n, total); break;
+    case 14: hipLaunchKernelGGL((k_copy_segments<Seg, 8, 4>), grid, block, 0, s, seg, n, total); break;
+    case 15: hipLaunchKernelGGL((k_copy_segments<Seg, 2, 4>), grid, block, 0, s, seg, n, total); break;
     default: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0>), grid, block, 0, s, seg, n, total); break;
     }
     return hipGetLastError();

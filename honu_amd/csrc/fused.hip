@@ -1,0 +1,401 @@
+// fused.hip — single-launch Metadata decode (honu_decode_records /
+// honu_decode_batch) and single-launch header + Metadata encode
+// (honu_marshal_records / honu_marshal_batch).
+//
+// The split pipelines (win.hip + scan.hip + grp.hip; grp.hip + scan.hip +
+// lane.hip) hand per-record counts, positions and offsets between five to
+// seven launches through the context scratch, and each later launch reads the
+// rows / ACL bytes again. Here one wave owns a tile of 64 consecutive
+// records (one per lane) from the first byte to the last: the wave walks or
+// sizes its records, the decoupled look-back (lookback.h) turns the counts
+// into table / output offsets, and the wave writes every output with those
+// offsets — rows and row fields once, ACL bytes re-read right after the walk
+// fetched them (L2-resident), no scratch round trips, no launch boundaries.
+#include <stdlib.h>
+
+#include "lookback.h"
+#include "win.h"
+
+namespace honu {
+
+#define OFF(f) ((int)offsetof(honu_meta, f))
+
+// Wave exclusive scan of v (64-bit); *total = the wave's sum.
+HONU_DEV uint64_t wave_excl(uint64_t v, uint64_t &total) {
+    const uint64_t inc = wave_inclusive_scan(v);
+    total = readlane64(inc, 63);
+    return inc - v;
+}
+
+// Largest lane r with pre(r) <= e, for pre non-decreasing over the lanes
+// (each lane its own e; pre read with ds_bpermute).
+HONU_DEV uint32_t lane_search(uint64_t pre, uint64_t e) {
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1) {
+        const uint32_t mid = lo + step;
+        const uint64_t v = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(pre >> 32), (int)mid) << 32) |
+                           (uint32_t)__shfl((int)(uint32_t)pre, (int)mid);
+        if (mid < 64 && v <= e) lo = mid;
+    }
+    return lo;
+}
+HONU_DEV uint64_t shfl64(uint64_t v, uint32_t src) {
+    return ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src) << 32) |
+           (uint32_t)__shfl((int)(uint32_t)v, (int)src);
+}
+
+// ------------------------------------------------------------------------
+// decode: Object.Metadata() + Data() + Tombstone() + StorageVersion()
+// (object.go:47-134), lani walk metadata.go:202-302, tables and offsets.
+// Columns: 0 ACL entries, 1 regions, 2 16-byte aligned payload bytes.
+// ------------------------------------------------------------------------
+struct DecodeOut {
+    honu_meta *meta;
+    honu_record_info *info;
+    honu_acl *acl;
+    uint64_t acl_cap;
+    uint32_t *reg;
+    uint64_t reg_cap;
+    uint64_t data_cap;
+    int materialize;          // data offsets into a data arena (else zero-copy)
+    DecodeScratch *scratch;   // materialize: payload sources for honu_decode_payloads
+    uint64_t *offs;           // materialize: offs[3i+2] = data arena offset
+    uint64_t *totals;         // column totals (3)
+    int dbg;                  // measurement knobs (HONU_FUSED_DBG): 1 no ACL fill, 2 no look-back wait
+};
+
+__global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
+    const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
+    DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t lb_words) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * WIN_WAVE_BYTES];
+    uint8_t *ws = smem + (threadIdx.x / HONU_WAVE) * WIN_WAVE_BYTES;
+    const uint32_t lane = lane_id();
+    const uint32_t ep = lb_epoch(lb);
+    const uint64_t ntiles = (n + HONU_WAVE - 1) / HONU_WAVE;
+    uint64_t t;
+    uint64_t k_static = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + threadIdx.x / HONU_WAVE;
+    for (;;) {
+        if (O.dbg & 4) {  // measurement only (with 2): static tiles, no tickets
+            t = k_static;
+            k_static += gridDim.x * HONU_WAVES_PER_BLOCK;
+        } else {
+            t = lb_ticket(lb);
+        }
+        if (t >= ntiles) break;
+        const uint64_t i0 = t * HONU_WAVE, i = i0 + lane;
+        const bool valid = i < n;
+        WinParse P;
+        win_walk(i0, ws, rec, rec_off, n, P);
+
+        // counts -> offsets: wave scan + look-back across tiles
+        const uint64_t c0 = P.nacl, c1 = P.nreg, c2 = (P.data_len + 15) & ~15ull;
+        uint64_t agg[3], excl[3];
+        const uint64_t x0 = wave_excl(c0, agg[0]);
+        const uint64_t x1 = wave_excl(c1, agg[1]);
+        const uint64_t x2 = wave_excl(c2, agg[2]);
+        if (O.dbg & 2) {
+            excl[0] = excl[1] = excl[2] = 0;
+        } else {
+            lb_scan<3>(lb_status, t, ep, agg, excl);
+        }
+        if (t == ntiles - 1 && lane < 3)
+            O.totals[lane] = lane == 0 ? excl[0] + agg[0] : (lane == 1 ? excl[1] + agg[1] : excl[2] + agg[2]);
+        const uint64_t ao = excl[0] + x0, ro = excl[1] + x1, doff = excl[2] + x2;
+
+        int32_t mst = P.st;
+        if (mst == HONU_OK) {  // as honu_decode_tables: offsets first, then the capacity check
+            if (P.nacl) P.R.u64(OFF(acl_off), ao);
+            if (P.nreg) P.R.u64(OFF(regions_off), ro);
+            if (ao + P.nacl > O.acl_cap || ro + P.nreg > O.reg_cap) mst = HONU_ERR_CAPACITY;
+        }
+        int32_t dst_ = P.data_status;
+        uint64_t doff_out = P.data_off, dlen_out = P.data_len;
+        if (O.materialize && dst_ == HONU_OK && P.data_len) {
+            if (doff + P.data_len > O.data_cap) {
+                dst_ = HONU_ERR_CAPACITY;
+                doff_out = dlen_out = 0;
+            } else {
+                doff_out = doff;
+            }
+        }
+        rows_out(ws, P.R, i0, n, O.meta);
+        if (valid) {
+            store_info(O.info + i, make_info(P, doff_out, dlen_out, dst_, mst));
+            if (O.materialize) {
+                O.scratch[i].data_src = P.data_off;
+                O.offs[3 * i + 2] = doff;
+            }
+        }
+
+        // region table: ids the walk kept in registers, else re-read
+        const bool ok = valid && mst == HONU_OK;
+        if (ok && P.nreg) {
+            if (P.reg_pos & GRP_REG_INLINE) {
+#pragma unroll
+                for (int k = 0; k < REG_INLINE; k++)
+                    if ((uint64_t)k < P.nreg) O.reg[ro + k] = P.regs[k];
+            } else {
+                uint64_t p = P.reg_pos & GRP_POS_MASK;
+                for (uint64_t k = 0; k < P.nreg; k++) {
+                    const uint64_t avail = P.end - p;
+                    uint64_t lo, hi, v = 0;
+                    lane_fetch16(rec, p, P.end, lo, hi);
+                    const uint32_t kk = uvarint_window(lo, hi, avail < 5 ? (uint32_t)avail : 5, v);
+                    O.reg[ro + k] = (uint32_t)v;
+                    p += kk;
+                }
+            }
+        }
+        // ACL table. Lists with every entry present: the wave's entries are one
+        // run of the table; lane e of a round takes entry e of that run (record
+        // by a search over the lanes' prefixes), reads the 17 bytes after its
+        // flag (the walk fetched them moments ago) and stores the 20-byte row.
+        const bool fast = ok && P.nacl && (P.acl_pos & GRP_ACL_FAST);
+        const uint64_t apos = P.acl_pos & GRP_POS_MASK;
+        if (ok && P.nacl && !fast) {  // nil entries: the lane walks its list (validated)
+            uint64_t p = apos;
+            for (uint64_t k = 0; k < P.nacl; k++) {
+                uint32_t *d = reinterpret_cast<uint32_t *>(O.acl + ao + k);
+                if (rec[p]) {
+                    uint64_t lo, hi;
+                    lane_fetch16(rec, p + 1, P.end, lo, hi);
+                    d[0] = (uint32_t)lo;
+                    d[1] = (uint32_t)(lo >> 32);
+                    d[2] = (uint32_t)hi;
+                    d[3] = (uint32_t)(hi >> 32);
+                    d[4] = rec[p + 17] | (1u << 8);
+                    p += 18;
+                } else {
+                    d[0] = d[1] = d[2] = d[3] = d[4] = 0;
+                    p += 1;
+                }
+            }
+        }
+        uint64_t ftot;
+        const uint64_t fpre = wave_excl(fast ? P.nacl : 0, ftot);
+        constexpr int U = 4;  // entries per lane in flight
+        if (!(O.dbg & 1))
+        for (uint64_t e0 = 0; e0 < ftot; e0 += U * HONU_WAVE) {  // wave-uniform
+            u32x4 a[U], b[U];
+            uint64_t dst[U];
+            uint32_t sh[U];
+#pragma unroll
+            for (int k = 0; k < U; k++) {
+                const uint64_t e = e0 + lane + HONU_WAVE * k;
+                const uint32_t r = lane_search(fpre, e < ftot ? e : 0);
+                const uint64_t rp = shfl64(fpre, r), ra = shfl64(apos, r), rao = shfl64(ao, r);
+                const uint64_t j = e - rp;
+                const uint64_t q = ra + 18 * j + 1;  // ClientID, then Permissions at q + 16
+                sh[k] = (uint32_t)(q & 15);
+                dst[k] = rao + j;
+                if (e < ftot) {
+                    a[k] = *reinterpret_cast<const u32x4 *>(rec + (q & ~15ull));
+                    b[k] = *reinterpret_cast<const u32x4 *>(rec + (q & ~15ull) + 16);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < U; k++) {
+                const uint64_t e = e0 + lane + HONU_WAVE * k;
+                if (e < ftot) {
+                    uint64_t lo, hi;
+                    window16(a[k], b[k], sh[k], lo, hi);
+                    const uint32_t s = sh[k];
+                    const uint32_t bw = s < 4 ? b[k].x : (s < 8 ? b[k].y : (s < 12 ? b[k].z : b[k].w));
+                    const uint32_t pm = (bw >> (8 * (s & 3))) & 0xFF;
+                    uint32_t *d = reinterpret_cast<uint32_t *>(O.acl + dst[k]);
+                    d[0] = (uint32_t)lo;
+                    d[1] = (uint32_t)(lo >> 32);
+                    d[2] = (uint32_t)hi;
+                    d[3] = (uint32_t)(hi >> 32);
+                    d[4] = pm | (1u << 8);
+                }
+            }
+        }
+    }
+    if (!(O.dbg & 4)) lb_finish(lb, lb_status, lb_words, t, ntiles, gridDim.x * HONU_WAVES_PER_BLOCK);
+}
+
+hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                               honu_meta *meta, honu_record_info *info, honu_acl *acl,
+                               uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap, int materialize,
+                               uint64_t data_cap, DecodeScratch *scratch, uint64_t *offs,
+                               uint64_t *totals, LbState *lb, uint64_t *lb_status,
+                               uint64_t lb_words, int max_blocks, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t tiles = (n + HONU_WAVE - 1) / HONU_WAVE;
+    uint64_t b = (tiles + HONU_WAVES_PER_BLOCK - 1) / HONU_WAVES_PER_BLOCK;
+    if (max_blocks > 0 && b > (uint64_t)max_blocks) b = (uint64_t)max_blocks;
+    static const int dbg = getenv("HONU_FUSED_DBG") ? atoi(getenv("HONU_FUSED_DBG")) : 0;
+    DecodeOut O{meta, info, acl, acl_cap, reg, reg_cap, data_cap, materialize, scratch, offs, totals, dbg};
+    hipLaunchKernelGGL(k_decode_fused, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
+                       O, lb, lb_status, lb_words);
+    return hipGetLastError();
+}
+
+
+// ------------------------------------------------------------------------
+// encode: object.Marshal (object.go:24-45) of every record except the payload
+// bytes: exact size, output offset (look-back), header + Metadata tail
+// (metadata.go:108-200). One column: the encoded bytes.
+// ------------------------------------------------------------------------
+#ifndef ENC_COUNT_U
+#define ENC_COUNT_U 16
+#endif
+#ifndef ENC_CHUNK_U
+#define ENC_CHUNK_U 4
+#endif
+constexpr uint32_t EROW = 368;                  // LDS stride of a staged row (92 dwords:
+                                                // the lanes of a ds_read_b128 hit distinct banks)
+constexpr uint32_t ESTAGE = 32 * EROW;          // half a tile of rows
+struct EncodeIn {
+    const honu_meta *meta;
+    const uint8_t *var;
+    uint64_t var_len;
+    const honu_acl *acl;
+    uint64_t acl_len;
+    const uint32_t *reg;
+    uint64_t reg_len;
+    const uint64_t *payload_off;
+};
+
+__global__ __launch_bounds__(HONU_BLOCK, 2) void k_encode_fused(
+    EncodeIn I, uint64_t n, uint8_t *__restrict__ out, uint64_t out_cap,
+    uint64_t *__restrict__ out_off, int32_t *__restrict__ status, LbState *lb,
+    uint64_t *lb_status, uint64_t lb_words) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * ESTAGE];
+    uint8_t *ws = smem + (threadIdx.x / HONU_WAVE) * ESTAGE;
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(ws);  // 64 counters, after the rows are read
+    const uint32_t lane = lane_id();
+    const uint32_t ep = lb_epoch(lb);
+    const uint64_t ntiles = (n + HONU_WAVE - 1) / HONU_WAVE;
+    uint64_t t;
+    for (;;) {
+        t = lb_ticket(lb);
+        if (t >= ntiles) break;
+        const uint64_t i0 = t * HONU_WAVE, i = i0 + lane;
+        const bool valid = i < n;
+        // the tile's rows: coalesced 16-byte loads -> LDS -> one row per lane
+        honu_meta m;
+        for (uint32_t h = 0; h < 2; h++) {
+            const uint64_t r0 = i0 + 32 * h;
+            const uint32_t rows = r0 >= n ? 0 : (uint32_t)(n - r0 < 32 ? n - r0 : 32);
+            const u32x4 *src = reinterpret_cast<const u32x4 *>(I.meta + r0);
+            wave_sync();
+            for (uint32_t s = lane; s < rows * 22; s += HONU_WAVE)
+                *reinterpret_cast<u32x4 *>(ws + (s / 22) * EROW + (s % 22) * 16) = src[s];
+            wave_sync();
+            if ((lane >> 5) == h) {
+                const u32x4 *row = reinterpret_cast<const u32x4 *>(ws + (lane & 31) * EROW);
+                u32x4 *dst = reinterpret_cast<u32x4 *>(&m);
+#pragma unroll
+                for (int c = 0; c < 22; c++) dst[c] = row[c];
+            }
+        }
+        wave_sync();
+        int32_t st = valid ? encode_check(m, I.var_len, I.acl_len, I.reg_len) : HONU_SKIP;
+        const uint64_t tail = st == HONU_OK ? encode_tail_bytes_noacl(m, I.reg) : 0;
+        // present ACL entries per record: the wave's lists as one run of
+        // entries (record by a search over the prefixes), counted in LDS
+        const uint64_t na = st == HONU_OK ? m.acl_count : 0, ao = m.acl_off;
+        uint64_t atot;
+        const uint64_t apre = wave_excl(na, atot);
+        cnt[lane] = 0;
+        wave_sync();
+        constexpr int UC = ENC_COUNT_U;  // entries per lane in flight
+        for (uint64_t e0 = 0; e0 < atot; e0 += UC * HONU_WAVE) {  // wave-uniform
+            uint32_t pz[UC], rr[UC];
+#pragma unroll
+            for (int k = 0; k < UC; k++) {
+                const uint64_t e = e0 + lane + HONU_WAVE * k;
+                const uint32_t r = lane_search(apre, e < atot ? e : 0);
+                rr[k] = r;
+                const uint64_t src = shfl64(ao, r) + (e - shfl64(apre, r));
+                pz[k] = e < atot ? I.acl[src].present : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < UC; k++)
+                if (pz[k]) atomicAdd(&cnt[rr[k]], 1u);
+        }
+        wave_sync();
+        const uint64_t present = cnt[lane];
+        const uint64_t dlen = valid ? I.payload_off[i + 1] - I.payload_off[i] : 0;
+        const uint64_t size = st == HONU_OK ? 1 + uvarint_len(dlen) + dlen + tail + na + 17 * present : 0;
+
+        // sizes -> output offsets: wave scan + look-back across tiles
+        uint64_t agg[1], excl[1];
+        const uint64_t x = wave_excl(size, agg[0]);
+        lb_scan<1>(lb_status, t, ep, agg, excl);
+        const uint64_t beg = excl[0] + x, end = beg + size;
+        if (t == ntiles - 1 && lane == 0) out_off[n] = excl[0] + agg[0];
+        if (st == HONU_OK && end > out_cap) st = HONU_ERR_CAPACITY;
+        if (valid) {
+            out_off[i] = beg;
+            status[i] = st;
+        }
+
+        // header + tail but the ACL entries (the lane), then the entries
+        uint64_t pos = 0;
+        if (st == HONU_OK) pos = encode_record_lane<true>(m, I.var, I.acl, I.reg, dlen, beg, end, out);
+        const bool all = st == HONU_OK && na && (pos & ACL_ALL_PRESENT);
+        const uint64_t P = pos & ~ACL_ALL_PRESENT;
+        if (st == HONU_OK && na && !all) {  // nil entries: 00, else 01 | ClientID | Permissions
+            uint64_t p = P;
+            for (uint64_t j = 0; j < na; j++) {
+                const honu_acl *a = I.acl + ao + j;
+                if (a->present) {
+                    uint32_t d[5];
+                    acl_enc_words(a, d);
+                    for (int b = 0; b < 18; b++) out[p + b] = (uint8_t)(d[b >> 2] >> (8 * (b & 3)));
+                    p += 18;
+                } else {
+                    out[p++] = 0;
+                }
+            }
+        }
+        // every entry present: the whole aligned 16-byte chunks of the lists
+        // [ceil16(P), floor16(P + 18 na)) as one run of chunks over the wave
+        const uint64_t X0 = (P + 15) & ~15ull, X1 = (P + 18 * na) & ~15ull;
+        const uint64_t nch = all && X1 > X0 ? (X1 - X0) >> 4 : 0;
+        uint64_t ctot;
+        const uint64_t cpre = wave_excl(nch, ctot);
+        constexpr int UK = ENC_CHUNK_U;  // chunks per lane in flight
+        for (uint64_t c0 = 0; c0 < ctot; c0 += UK * HONU_WAVE) {  // wave-uniform
+            u32x4 v[UK];
+            uint64_t dst[UK];
+#pragma unroll
+            for (int k = 0; k < UK; k++) {
+                const uint64_t c = c0 + lane + HONU_WAVE * k;
+                const uint32_t r = lane_search(cpre, c < ctot ? c : 0);
+                const uint64_t rP = shfl64(P, r), rX0 = shfl64(X0, r), rna = shfl64(na, r),
+                               rao = shfl64(ao, r);
+                dst[k] = rX0 + 16 * (c - shfl64(cpre, r));
+                if (c < ctot) v[k] = acl_chunk(I.acl + rao, rna, rP, dst[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < UK; k++)
+                if (c0 + lane + HONU_WAVE * k < ctot) *reinterpret_cast<u32x4 *>(out + dst[k]) = v[k];
+        }
+    }
+    lb_finish(lb, lb_status, lb_words, t, ntiles, gridDim.x * HONU_WAVES_PER_BLOCK);
+}
+
+hipError_t launch_encode_fused(const honu_meta *meta, const uint8_t *var, uint64_t var_len,
+                               const honu_acl *acl, uint64_t acl_len, const uint32_t *reg,
+                               uint64_t reg_len, const uint64_t *payload_off, uint64_t n,
+                               uint8_t *out, uint64_t out_cap, uint64_t *out_off, int32_t *status,
+                               LbState *lb, uint64_t *lb_status, uint64_t lb_words,
+                               int max_blocks, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t tiles = (n + HONU_WAVE - 1) / HONU_WAVE;
+    uint64_t b = (tiles + HONU_WAVES_PER_BLOCK - 1) / HONU_WAVES_PER_BLOCK;
+    if (max_blocks > 0 && b > (uint64_t)max_blocks) b = (uint64_t)max_blocks;
+    EncodeIn I{meta, var, var_len, acl, acl_len, reg, reg_len, payload_off};
+    hipLaunchKernelGGL(k_encode_fused, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, I, n, out,
+                       out_cap, out_off, status, lb, lb_status, lb_words);
+    return hipGetLastError();
+}
+
+#undef OFF
+
+}  // namespace honu

@@ -932,39 +932,6 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_grp(
 // loads, one aligned store per chunk, byte stores only at the list's ends.
 // A list with nil entries is written serially by the group's lead lane.
 // ------------------------------------------------------------------------
-// 16 output bytes at absolute X >= P of the list at P (every entry present)
-HONU_DEV u32x4 acl_chunk(const honu_acl *A, uint64_t na, uint64_t P, uint64_t X) {
-    const uint64_t j0 = (X - P) / 18;
-    uint32_t b[10];
-    acl_enc_words(A + j0, b);
-    b[5] = b[6] = b[7] = b[8] = b[9] = 0;
-    if (j0 + 1 < na) {  // entry j0 + 1 starts at byte 18 of b
-        uint32_t d[5];
-        acl_enc_words(A + j0 + 1, d);
-        b[4] = (b[4] & 0xFFFF) | (d[0] << 16);
-        b[5] = (d[0] >> 16) | (d[1] << 16);
-        b[6] = (d[1] >> 16) | (d[2] << 16);
-        b[7] = (d[2] >> 16) | (d[3] << 16);
-        b[8] = (d[3] >> 16) | (d[4] << 16);
-    }
-    // chunk byte k = byte (X - P - 18 j0) + k of b (X >= P)
-    const uint32_t off = (uint32_t)(X - (P + 18 * j0));
-    const uint32_t q = off >> 2, sh = off & 3;
-    uint32_t o[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        uint32_t w0 = b[k], w1 = b[k + 1];
-#pragma unroll
-        for (int t = 1; t <= 4; t++)
-            if ((uint32_t)t == q) {
-                w0 = b[t + k];
-                w1 = b[t + k + 1];
-            }
-        o[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-    }
-    return u32x4{o[0], o[1], o[2], o[3]};
-}
-
 template <int G>
 HONU_DEV void k_encode_acl_grp_one(uint64_t i, const honu_meta *__restrict__ meta, const honu_acl *__restrict__ acl, uint64_t n,
     uint8_t *__restrict__ out, const int32_t *__restrict__ status,

@@ -4,6 +4,7 @@
 #pragma once
 
 #include "common.h"
+#include "lookback.h"
 
 // LDS budget per wave for the Metadata tail writer (encode.hip) and the
 // decode window (decode.hip). Generated tails are 0.15-1.8 KB; longer tails
@@ -41,6 +42,39 @@ HONU_DEV void acl_enc_words(const honu_acl *e, uint32_t d[5]) {
     d[2] = (e1 >> 24) | (e2 << 8);
     d[3] = (e2 >> 24) | (e3 << 8);
     d[4] = (e3 >> 24) | ((e4 & 0xFF) << 8);
+}
+
+// 16 output bytes at absolute X >= P of the list at P (every entry present)
+HONU_DEV u32x4 acl_chunk(const honu_acl *A, uint64_t na, uint64_t P, uint64_t X) {
+    const uint64_t j0 = (X - P) / 18;
+    uint32_t b[10];
+    acl_enc_words(A + j0, b);
+    b[5] = b[6] = b[7] = b[8] = b[9] = 0;
+    if (j0 + 1 < na) {  // entry j0 + 1 starts at byte 18 of b
+        uint32_t d[5];
+        acl_enc_words(A + j0 + 1, d);
+        b[4] = (b[4] & 0xFFFF) | (d[0] << 16);
+        b[5] = (d[0] >> 16) | (d[1] << 16);
+        b[6] = (d[1] >> 16) | (d[2] << 16);
+        b[7] = (d[2] >> 16) | (d[3] << 16);
+        b[8] = (d[3] >> 16) | (d[4] << 16);
+    }
+    // chunk byte k = byte (X - P - 18 j0) + k of b (X >= P)
+    const uint32_t off = (uint32_t)(X - (P + 18 * j0));
+    const uint32_t q = off >> 2, sh = off & 3;
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        uint32_t w0 = b[k], w1 = b[k + 1];
+#pragma unroll
+        for (int t = 1; t <= 4; t++)
+            if ((uint32_t)t == q) {
+                w0 = b[t + k];
+                w1 = b[t + k + 1];
+            }
+        o[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    }
+    return u32x4{o[0], o[1], o[2], o[3]};
 }
 
 struct LaunchGeom {
@@ -132,6 +166,22 @@ hipError_t launch_decode_fill_grp(const uint8_t *rec, uint64_t n, honu_meta *met
                                   const uint64_t *offs, honu_acl *acl, uint64_t acl_cap,
                                   uint32_t *reg, uint64_t reg_cap, uint8_t *data,
                                   uint64_t data_cap, int max_blocks, hipStream_t s);
+
+// fused.hip: one launch from records to rows, record info and tables
+// (materialize: also the data-arena offsets honu_decode_payloads copies to)
+hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
+                               honu_meta *meta, honu_record_info *info, honu_acl *acl,
+                               uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap, int materialize,
+                               uint64_t data_cap, DecodeScratch *scratch, uint64_t *offs,
+                               uint64_t *totals, LbState *lb, uint64_t *lb_status,
+                               uint64_t lb_words, int max_blocks, hipStream_t s);
+
+hipError_t launch_encode_fused(const honu_meta *meta, const uint8_t *var, uint64_t var_len,
+                               const honu_acl *acl, uint64_t acl_len, const uint32_t *reg,
+                               uint64_t reg_len, const uint64_t *payload_off, uint64_t n,
+                               uint8_t *out, uint64_t out_cap, uint64_t *out_off, int32_t *status,
+                               LbState *lb, uint64_t *lb_status, uint64_t lb_words,
+                               int max_blocks, hipStream_t s);
 
 hipError_t launch_decode_parse_win(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                    honu_meta *meta, honu_record_info *info,

@@ -316,76 +316,25 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_lane(
 // ------------------------------------------------------------------------
 // encode size pass: exact record length (object.go:24-45 / App. A)
 // ------------------------------------------------------------------------
-HONU_DEV bool span_in(uint64_t off, uint64_t len, uint64_t var_len) {
-    return len == 0 || (off <= var_len && len <= var_len - off);
-}
-HONU_DEV uint64_t frame_len(uint64_t len) { return uvarint_len(len) + len; }
-
 HONU_DEV void k_encode_sizes_lane_one(uint64_t i, const honu_meta *__restrict__ meta, uint64_t var_len, const honu_acl *__restrict__ acl,
     uint64_t acl_len, const uint32_t *__restrict__ reg, uint64_t reg_len,
     const uint64_t *__restrict__ payload_off, uint64_t n, uint64_t *__restrict__ sizes,
     int32_t *__restrict__ status) {
     const honu_meta &m = meta[i];
-    const uint32_t pr = m.present;
     uint64_t size = 0;
-    int32_t st = HONU_OK;
-    if (!(pr & HONU_HAS_META)) {
-        st = HONU_ERR_PANIC;  // Marshal(nil, ...): nil deref in Size(), metadata.go:66
-    } else {
-        bool ok = span_in(m.mime.off, m.mime.len, var_len);
-        if (pr & HONU_HAS_SCHEMA) ok = ok && span_in(m.schema_name.off, m.schema_name.len, var_len);
-        if (pr & HONU_HAS_PUBLISHER)
-            ok = ok && span_in(m.ip_address.off, m.ip_address.len, var_len) &&
-                 span_in(m.user_agent.off, m.user_agent.len, var_len);
-        if (pr & HONU_HAS_ENCRYPTION)
-            ok = ok && span_in(m.public_key_id.off, m.public_key_id.len, var_len) &&
-                 span_in(m.encryption_key.off, m.encryption_key.len, var_len) &&
-                 span_in(m.hmac_secret.off, m.hmac_secret.len, var_len) &&
-                 span_in(m.signature.off, m.signature.len, var_len);
-        const uint64_t na = m.acl_count, nr = m.regions_count;
-        const uint64_t ao = m.acl_off, ro = m.regions_off;
-        if (na) ok = ok && ao <= acl_len && na <= acl_len - ao;
-        if (nr) ok = ok && ro <= reg_len && nr <= reg_len - ro;
-        if (!ok) {
-            st = HONU_ERR_INPUT;
-        } else {
-            uint64_t t = 1 + 32;  // meta flag, ObjectID, CollectionID
-            t += 1;               // Version flag
-            if (pr & HONU_HAS_VERSION)
-                t += uvarint_len(m.pid) + uvarint_len(m.vid) + uvarint_len(m.region) + 1 +
-                     ((pr & HONU_HAS_PARENT) ? uvarint_len(m.parent_pid) + uvarint_len(m.parent_vid) : 0) +
-                     1 + uvarint_len(zigzag(m.version_created));
-            t += 1;  // Schema flag
-            if (pr & HONU_HAS_SCHEMA)
-                t += frame_len(m.schema_name.len) + uvarint_len(m.schema_major) +
-                     uvarint_len(m.schema_minor) + uvarint_len(m.schema_patch);
-            t += frame_len(m.mime.len) + 33;  // MIME, Owner, Group, Permissions
-            t += uvarint_len(na);
-            for (uint64_t k0 = 0; k0 < na; k0 += 8) {  // 8 independent loads per round
-                uint32_t pz[8];
+    const int32_t st = encode_check(m, var_len, acl_len, reg_len);
+    if (st == HONU_OK) {
+        const uint64_t na = m.acl_count, ao = m.acl_off;
+        uint64_t t = encode_tail_bytes_noacl(m, reg);
+        for (uint64_t k0 = 0; k0 < na; k0 += 8) {  // 8 independent loads per round
+            uint32_t pz[8];
 #pragma unroll
-                for (int j = 0; j < 8; j++) pz[j] = k0 + j < na ? acl[ao + k0 + j].present : 2;
+            for (int j = 0; j < 8; j++) pz[j] = k0 + j < na ? acl[ao + k0 + j].present : 2;
 #pragma unroll
-                for (int j = 0; j < 8; j++) t += pz[j] == 2 ? 0 : (pz[j] ? 18 : 1);
-            }
-            t += uvarint_len(nr);
-            for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
-                uint32_t r8[8];
-#pragma unroll
-                for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? reg[ro + k0 + j] : 0;
-#pragma unroll
-                for (int j = 0; j < 8; j++) t += k0 + j < nr ? uvarint_len(r8[j]) : 0;
-            }
-            t += 3;  // Publisher, Encryption, Compression flags
-            if (pr & HONU_HAS_PUBLISHER) t += 32 + frame_len(m.ip_address.len) + frame_len(m.user_agent.len);
-            if (pr & HONU_HAS_ENCRYPTION)
-                t += frame_len(m.public_key_id.len) + frame_len(m.encryption_key.len) +
-                     frame_len(m.hmac_secret.len) + frame_len(m.signature.len) + 3;
-            if (pr & HONU_HAS_COMPRESSION) t += 1 + uvarint_len(zigzag(m.compression_level));
-            t += 1 + uvarint_len(zigzag(m.created)) + uvarint_len(zigzag(m.modified));
-            const uint64_t dlen = payload_off[i + 1] - payload_off[i];
-            size = 1 + uvarint_len(dlen) + dlen + t;  // object.go:30,35,40
+            for (int j = 0; j < 8; j++) t += pz[j] == 2 ? 0 : (pz[j] ? 18 : 1);
         }
+        const uint64_t dlen = payload_off[i + 1] - payload_off[i];
+        size = 1 + uvarint_len(dlen) + dlen + t;  // object.go:30,35,40
     }
     sizes[i] = size;
     if (status) status[i] = st;
@@ -404,11 +353,6 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_sizes_lane(
 // ------------------------------------------------------------------------
 // encode: header + Metadata tail (object.go:24-45, metadata.go:108-200)
 // ------------------------------------------------------------------------
-HONU_DEV uint64_t ld64(const uint8_t *p) { return *reinterpret_cast<const uint64_t *>(p); }
-
-// SKIP_ACL: leave the ACL entries to k_encode_acl_grp (grp.hip): write the
-// fields up to uvarint(len ACL), record that position in acl_out[i], and
-// resume at end - (bytes after the list), computed from the row and regions.
 template <bool SKIP_ACL>
 HONU_DEV void k_encode_meta_lane_one(uint64_t i, const honu_meta *__restrict__ meta, const uint8_t *__restrict__ var,
     const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
@@ -429,168 +373,9 @@ HONU_DEV void k_encode_meta_lane_one(uint64_t i, const honu_meta *__restrict__ m
 #pragma unroll
         for (int k = 0; k < 22; k++) dstr[k] = src[k];
     }
-    const uint8_t *mb = reinterpret_cast<const uint8_t *>(&m);
-    const uint32_t pr = m.present;
     const uint64_t dlen = payload_off[i + 1] - payload_off[i];
-    {  // header: version byte + uvarint(len data)   object.go:30,35
-        uint64_t lo, hi;
-        const uint32_t hn = uvarint_bytes(dlen, lo, hi);
-        out[beg] = HONU_STORAGE_VERSION;
-        for (uint32_t j = 0; j < hn; j++)
-            out[beg + 1 + j] = (uint8_t)(j < 8 ? lo >> (8 * j) : hi >> (8 * (j - 8)));
-    }
-    LaneWriter W;
-    W.init(out, beg + 1 + uvarint_len(dlen) + dlen);
-    W.byte(1);                                                      // EncodeStruct(meta)
-    W.put16(ld64(mb + OFF(object_id)), ld64(mb + OFF(object_id) + 8));          // :110
-    W.put16(ld64(mb + OFF(collection_id)), ld64(mb + OFF(collection_id) + 8));  // :115
-    if (pr & HONU_HAS_VERSION) {                                    // :120, version.go:44-70
-        W.byte(1);
-        W.uv(m.pid);
-        W.uv(m.vid);
-        W.uv(m.region);
-        if (pr & HONU_HAS_PARENT) {
-            W.byte(1);
-            W.uv(m.parent_pid);
-            W.uv(m.parent_vid);
-        } else {
-            W.byte(0);
-        }
-        W.byte(m.tombstone ? 1 : 0);
-        W.uv(zigzag(m.version_created));
-    } else {
-        W.byte(0);
-    }
-    if (pr & HONU_HAS_SCHEMA) {                                     // :125, schema.go:30-53
-        W.byte(1);
-        W.frame(var, m.schema_name);
-        W.uv(m.schema_major);
-        W.uv(m.schema_minor);
-        W.uv(m.schema_patch);
-    } else {
-        W.byte(0);
-    }
-    W.frame(var, m.mime);                                           // :130
-    W.put16(ld64(mb + OFF(owner)), ld64(mb + OFF(owner) + 8));      // :135
-    W.put16(ld64(mb + OFF(group)), ld64(mb + OFF(group) + 8));      // :140
-    W.byte(m.permissions);                                          // :145
-    const uint64_t na = m.acl_count, ao = m.acl_off;
-    W.uv(na);                                                       // :151
-    const uint64_t nr = m.regions_count, ro = m.regions_off;
-    if constexpr (SKIP_ACL) {
-        const uint64_t P = W.pos();
-        uint64_t sfx = uvarint_len(nr) + 3 + 1 + uvarint_len(zigzag(m.created)) +
-                       uvarint_len(zigzag(m.modified));
-        for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
-            uint32_t r8[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? reg[ro + k0 + j] : 0;
-#pragma unroll
-            for (int j = 0; j < 8; j++) sfx += k0 + j < nr ? uvarint_len(r8[j]) : 0;
-        }
-        if (pr & HONU_HAS_PUBLISHER) sfx += 32 + frame_len(m.ip_address.len) + frame_len(m.user_agent.len);
-        if (pr & HONU_HAS_ENCRYPTION)
-            sfx += frame_len(m.public_key_id.len) + frame_len(m.encryption_key.len) +
-                   frame_len(m.hmac_secret.len) + frame_len(m.signature.len) + 3;
-        if (pr & HONU_HAS_COMPRESSION) sfx += 1 + uvarint_len(zigzag(m.compression_level));
-        const uint64_t E = end - sfx;  // the list is [P, E)
-        if (na && E - P == 18 * na) {
-            // every entry present (a nil entry is 1 byte): this lane writes the
-            // list's bytes in the partial 16-byte chunks at both ends, so the
-            // group kernel stores whole aligned chunks only
-            acl_out[i] = P | ACL_ALL_PRESENT;
-            const uint64_t hend = ((P + 15) & ~15ull) < E ? ((P + 15) & ~15ull) : E;
-            const uint64_t T = (E & ~15ull) > hend ? (E & ~15ull) : hend;
-            for (uint64_t x = P; x < E;) {
-                if (x == hend && x < T) {
-                    W.jump(T);
-                    x = T;
-                    continue;
-                }
-                const uint64_t j = (x - P) / 18;
-                uint32_t d[5];
-                acl_enc_words(acl + ao + j, d);
-                const uint64_t lo = ((uint64_t)d[1] << 32) | d[0], hi = ((uint64_t)d[3] << 32) | d[2];
-                const uint64_t stop = P + 18 * (j + 1) < (x < hend ? hend : E) ? P + 18 * (j + 1)
-                                                                             : (x < hend ? hend : E);
-                for (; x < stop; x++) {
-                    const uint32_t k = (uint32_t)(x - P - 18 * j);
-                    const uint32_t bv = k < 8 ? (uint32_t)(lo >> (8 * k))
-                                              : k < 16 ? (uint32_t)(hi >> (8 * (k - 8)))
-                                                       : d[4] >> (8 * (k - 16));
-                    W.byte(bv);
-                }
-            }
-        } else {
-            acl_out[i] = P;
-            W.jump(E);
-        }
-    } else {
-    for (uint64_t k0 = 0; k0 < na; k0 += 8) {                       // :157-162, acls.go:26-39
-        uint32_t e[8][5];                                            // 8 entries ahead
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            if (k0 + j < na) {
-                const uint32_t *a = reinterpret_cast<const uint32_t *>(acl + ao + k0 + j);
-#pragma unroll
-                for (int c = 0; c < 5; c++) e[j][c] = a[c];
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            if (k0 + j < na) {
-                if ((e[j][4] >> 8) & 0xFF) {
-                    W.byte(1);
-                    W.put16(((uint64_t)e[j][1] << 32) | e[j][0], ((uint64_t)e[j][3] << 32) | e[j][2]);
-                    W.byte(e[j][4]);
-                } else {
-                    W.byte(0);
-                }
-            }
-        }
-    }
-    }
-    W.uv(nr);                                                       // :164, region.go:137-152
-    for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
-        uint32_t r8[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? reg[ro + k0 + j] : 0;
-#pragma unroll
-        for (int j = 0; j < 8; j++)
-            if (k0 + j < nr) W.uv(r8[j]);
-    }
-    if (pr & HONU_HAS_PUBLISHER) {                                  // :169, provenance.go:34-57
-        W.byte(1);
-        W.put16(ld64(mb + OFF(publisher_id)), ld64(mb + OFF(publisher_id) + 8));
-        W.put16(ld64(mb + OFF(client_id)), ld64(mb + OFF(client_id) + 8));
-        W.frame(var, m.ip_address);
-        W.frame(var, m.user_agent);
-    } else {
-        W.byte(0);
-    }
-    if (pr & HONU_HAS_ENCRYPTION) {                                 // :174, encryption.go:51-89
-        W.byte(1);
-        W.frame(var, m.public_key_id);
-        W.frame(var, m.encryption_key);
-        W.frame(var, m.hmac_secret);
-        W.frame(var, m.signature);
-        W.byte(m.sealing_alg);
-        W.byte(m.encryption_alg);
-        W.byte(m.signature_alg);
-    } else {
-        W.byte(0);
-    }
-    if (pr & HONU_HAS_COMPRESSION) {                                // :179, compression.go:40-53
-        W.byte(1);
-        W.byte(m.compression_alg);
-        W.uv(zigzag(m.compression_level));
-    } else {
-        W.byte(0);
-    }
-    W.byte(m.flags);                                                // :184
-    W.uv(zigzag(m.created));                                        // :189
-    W.uv(zigzag(m.modified));                                       // :194
-    W.finish();
+    const uint64_t pos = encode_record_lane<SKIP_ACL>(m, var, acl, reg, dlen, beg, end, out);
+    if constexpr (SKIP_ACL) acl_out[i] = pos;
 }
 
 template <bool SKIP_ACL>

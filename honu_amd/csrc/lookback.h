@@ -1,0 +1,138 @@
+// lookback.h — single-pass exclusive scan across a launch (decoupled
+// look-back) for the fused codec kernels: one TILE per wave (64 records, one
+// per lane), tiles handed out in order by an atomic ticket, so a wave that
+// waits on an earlier tile waits on a wave that is already running.
+//
+// Every tile publishes, per column, a 64-bit status word: its aggregate as
+// soon as its own records are counted, then its inclusive prefix once the
+// look-back has found it. A waiting wave reads the 64 preceding tiles' words
+// at once (one per lane), sums back to the nearest inclusive prefix and
+// spins only while a tile in between has not published.
+//
+// Status word: bits 63:62 flag (0 none, 1 aggregate, 2 inclusive), 61:44 the
+// launch epoch (18 bits), 43:0 the value (< 2^44: the counts are bounded by the
+// bytes of one arena). Words of earlier launches carry another epoch, so the
+// array is never cleared between launches; the last wave of a launch resets
+// the ticket, advances the epoch and, when the epoch wraps, clears the array.
+// Launch at most as many waves as fit the chip at once: every ticket is one
+// atomic on one address, so tickets should be few per wave, not per tile.
+// Nothing is passed from the host per launch, so the kernels replay from a
+// captured hipGraph.
+#pragma once
+
+#include "common.h"
+
+namespace honu {
+
+struct LbState {
+    uint32_t ticket;  // next tile
+    uint32_t _unused;
+    uint32_t epoch;
+    uint32_t _pad;
+};
+
+constexpr uint32_t LB_EPOCH_BITS = 18;
+constexpr uint32_t LB_EPOCH_MASK = (1u << LB_EPOCH_BITS) - 1;
+constexpr uint64_t LB_VAL_MASK = (1ull << 44) - 1;
+
+HONU_DEV uint64_t lb_word(uint32_t flag, uint32_t epoch, uint64_t v) {
+    return ((uint64_t)flag << 62) | ((uint64_t)(epoch & LB_EPOCH_MASK) << 44) | (v & LB_VAL_MASK);
+}
+HONU_DEV uint64_t lb_load(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+HONU_DEV void lb_store(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The launch's epoch (wave-uniform; only the launch's last wave changes it).
+HONU_DEV uint32_t lb_epoch(LbState *s) {
+    return uniform32(__hip_atomic_load(&s->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Next tile for this wave (wave-uniform).
+HONU_DEV uint64_t lb_ticket(LbState *s) {
+    uint32_t t = 0;
+    if (lane_id() == 0)
+        t = __hip_atomic_fetch_add(&s->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readlane(t, 0);
+}
+
+// Tile t of the launch with per-column aggregates agg[c] (wave-uniform):
+// publishes them, returns the exclusive prefixes of the tile in excl[c] and
+// publishes the inclusive ones. status holds K words per tile.
+template <int K>
+HONU_DEV void lb_scan(uint64_t *status, uint64_t t, uint32_t ep, const uint64_t (&agg)[K],
+                      uint64_t (&excl)[K]) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int c = 0; c < K; c++) excl[c] = 0;
+    if (t == 0) {
+#pragma unroll
+        for (int c = 0; c < K; c++)
+            if (lane == (uint32_t)c) lb_store(status + c, lb_word(2, ep, agg[c]));
+        return;
+    }
+#pragma unroll
+    for (int c = 0; c < K; c++)
+        if (lane == (uint32_t)c) lb_store(status + t * K + c, lb_word(1, ep, agg[c]));
+    int64_t top[K];
+    bool done[K];
+#pragma unroll
+    for (int c = 0; c < K; c++) {
+        top[c] = (int64_t)t - 1;
+        done[c] = false;
+    }
+    for (;;) {
+        bool all = true;
+#pragma unroll
+        for (int c = 0; c < K; c++) {
+            if (done[c]) continue;
+            const int64_t idx = top[c] - (int64_t)lane;  // lane 0: the nearest tile
+            const uint64_t w = idx >= 0 ? lb_load(status + (uint64_t)idx * K + c)
+                                        : lb_word(2, ep, 0);  // before tile 0: prefix 0
+            const uint32_t fl = (uint32_t)(w >> 62);
+            const bool ready = fl != 0 && ((uint32_t)(w >> 44) & LB_EPOCH_MASK) == (ep & LB_EPOCH_MASK);
+            const uint64_t nb = __ballot(!ready);
+            const uint64_t ib = __ballot(ready && fl == 2);
+            const uint32_t p = ib ? (uint32_t)__builtin_ctzll(ib) : 64;  // nearest inclusive
+            const uint64_t upto = p >= 63 ? ~0ull : ((2ull << p) - 1);   // lanes 0..p
+            if (nb & upto) {  // a tile in between has not published yet
+                all = false;
+                continue;
+            }
+            excl[c] += wave_sum(lane <= p ? (w & LB_VAL_MASK) : 0);
+            if (p < 64) {
+                done[c] = true;
+            } else {
+                top[c] -= 64;
+                all = false;
+            }
+        }
+        if (all) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int c = 0; c < K; c++)
+        if (lane == (uint32_t)c) lb_store(status + t * K + c, lb_word(2, ep, excl[c] + agg[c]));
+}
+
+// Called by every wave with the ticket that ended its loop (t_end >= ntiles):
+// a wave takes that ticket only after finishing its last tile, so the wave
+// holding ticket ntiles + waves - 1 is the last one of the launch. It resets
+// the ticket and advances the epoch; on a wrap of the epoch it clears the
+// status array (status_words words) first.
+HONU_DEV void lb_finish(LbState *s, uint64_t *status, uint64_t status_words, uint64_t t_end,
+                        uint64_t ntiles, uint32_t waves) {
+    if (t_end != ntiles + waves - 1) return;
+    const uint32_t lane = lane_id();
+    const uint32_t e = (lb_epoch(s) + 1) & LB_EPOCH_MASK;
+    if (e == 0)
+        for (uint64_t k = lane; k < status_words; k += HONU_WAVE) lb_store(status + k, 0);
+    if (lane == 0) {
+        __hip_atomic_store(&s->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&s->epoch, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+}  // namespace honu

@@ -1,398 +1,11 @@
-// win.hip — decode parse with one record per LANE reading through per-lane
-// LDS windows (record_variant 0).
-//
-// One record per lane keeps the serial lani walk cheap (64 records per
-// wave-instruction stream), but a lane that fetches its own bytes makes every
-// load instruction touch 64 cache lines (one per record): measured TA-bound,
-// ~50 L1 tag lookups per load instruction and 3-6x L2 read amplification.
-// Here the wave moves each lane's next 256 bytes into a per-lane LDS window
-// with global_load_lds (16 slots of 16 B per window, 16 consecutive lanes of
-// one instruction read one record's 256 contiguous bytes), and the lanes walk
-// from LDS. Windows are refilled at fixed points of the grammar where the
-// whole wave is converged: the start of the tail, every ~14 ACL entries while
-// the entry flags are checked, after the ACL list and after the signature.
-// A field outside the lane's window is read from global memory, so the window
-// placement only affects speed, never results. Rows leave through LDS as
-// contiguous 16-byte stores (32 rows per pass).
-#include "kernels.h"
-#include "lane.h"
+// win.hip — the split decode parse (honu_decode_parse, record_variant 0):
+// one record per LANE reading through per-lane LDS windows (win.h). Rows go
+// out through LDS; the per-record list positions, counts and inline region ids
+// go to the context scratch for honu_decode_tables (scan + group fill).
+#include "win.h"
 
 namespace honu {
 
-#define GO_MAX_ALLOC (1ull << 48)  // runtime maxAlloc, linux/amd64
-#define OFF(f) ((int)offsetof(honu_meta, f))
-
-constexpr uint32_t WB = 256;           // window bytes per lane
-constexpr uint32_t WSL = WB / 16 + 1;  // LDS stride in 16-byte slots: one pad slot per
-                                       // window puts the lanes of a ds_read_b128 group
-                                       // on different banks
-constexpr uint32_t WS = WSL * 16;
-constexpr uint64_t NOWIN = ~0ull;
-constexpr uint32_t WIN_WAVE_BYTES = HONU_WAVE * WS + HONU_WAVE * 8;  // windows + wants
-
-struct LaneWin {
-    uint8_t *wave;      // this wave's windows (LDS)
-    uint64_t *wants;    // 64 requested bases (LDS)
-    const uint8_t *rec;
-    uint64_t lim;       // arena end: 16-byte blocks starting below it are mapped
-    uint64_t wb;        // absolute offset of this lane's window byte 0, NOWIN if none
-    uint32_t lane;
-
-    HONU_DEV const uint8_t *mine() const { return wave + lane * WS; }
-
-    // All 64 lanes: lane L's window becomes [want_L, want_L + WB) unless
-    // want_L == NOWIN (want 16-aligned). Slot s of the wave's window array is
-    // window s / WSL, block s % WSL; instruction k writes slots 64k .. 64k+63.
-    HONU_DEV void refill(uint64_t want) {
-        wants[lane] = want;
-        wave_sync();
-#pragma unroll
-        for (uint32_t k = 0; k < WSL; k++) {
-            const uint32_t s = 64 * k + lane;
-            const uint32_t L = s / WSL, c = s % WSL;
-            const uint64_t b = wants[L];
-            const uint64_t a = b + 16ull * c;
-            if (c < WB / 16 && b != NOWIN && a < lim)
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void *)(rec + a),
-                    (__attribute__((address_space(3))) void *)(wave + 1024 * k), 16, 0, 0);
-        }
-        __builtin_amdgcn_s_waitcnt(0);
-        wave_sync();
-        if (want != NOWIN) wb = want;
-    }
-    HONU_DEV bool has16(uint64_t p) const { return wb != NOWIN && p >= wb && p - wb <= WB - 16; }
-    // The LDS and the global read stay two instructions of their own address
-    // spaces: a select between the two pointers compiles to flat_load_ubyte
-    // (counted by both vmcnt and lgkmcnt, LDS hits at flat latency).
-    HONU_DEV uint32_t u8(uint64_t p) const {
-        if (wb != NOWIN && p >= wb && p - wb < WB)
-            return ((const __attribute__((address_space(3))) uint8_t *)mine())[p - wb];
-        return ((const __attribute__((address_space(1))) uint8_t *)rec)[p];
-    }
-    HONU_DEV void fetch16(uint64_t p, uint64_t end, uint64_t &lo, uint64_t &hi) const {
-        if (has16(p)) {
-            const uint32_t x = (uint32_t)(p - wb);
-            const u32x4 *b = reinterpret_cast<const u32x4 *>(mine() + (x & ~15u));
-            window16(b[0], b[1], x & 15, lo, hi);
-        } else {
-            lane_fetch16(rec, p, end, lo, hi);
-        }
-    }
-};
-
-struct WDec {  // lani.Decoder (lani/decode.go) over [tstart, end), as LaneDec
-    const LaneWin *w;
-    uint64_t p, end, tstart;
-
-    HONU_DEV int u8(uint32_t &v) {  // DecodeByte :94-103
-        if (p >= end) return HONU_ERR_EOF;
-        v = w->u8(p);
-        p += 1;
-        return HONU_OK;
-    }
-    HONU_DEV int boolean(uint32_t &v) {  // DecodeBool :105-120
-        int st = u8(v);
-        if (st) return st;
-        return v > 1 ? HONU_ERR_PARSE_BOOLEAN : HONU_OK;
-    }
-    HONU_DEV int uv(uint32_t maxw, int err, uint64_t &v) {
-        if (p >= end) return HONU_ERR_EOF;
-        const uint64_t avail = end - p;
-        const uint32_t n = avail < maxw ? (uint32_t)avail : maxw;
-        uint64_t lo, hi;
-        w->fetch16(p, end, lo, hi);
-        const uint32_t k = uvarint_window(lo, hi, n, v);
-        if (!k) return err;
-        p += k;
-        return HONU_OK;
-    }
-    HONU_DEV int u32(uint32_t &v) {  // DecodeUint32 :127-146
-        uint64_t x = 0;
-        int st = uv(5, HONU_ERR_PARSE_VARINT, x);
-        v = (uint32_t)x;
-        return st;
-    }
-    HONU_DEV int u64(uint64_t &v) { return uv(10, HONU_ERR_PARSE_VARINT, v); }  // :149-168
-    HONU_DEV int i64(int64_t &v) {                                             // :171-190
-        uint64_t x = 0;
-        int st = uv(10, HONU_ERR_PARSE_VARINT, x);
-        v = unzigzag(x);
-        return st;
-    }
-    HONU_DEV int ulid(uint64_t &lo, uint64_t &hi) {  // DecodeULID :209-221
-        if (p >= end) return HONU_ERR_EOF;
-        if (p + 16 > end) return HONU_ERR_UNEXPECTED_EOF;
-        w->fetch16(p, end, lo, hi);
-        p += 16;
-        return HONU_OK;
-    }
-    HONU_DEV int frame(uint64_t &off, uint64_t &len) {  // Decode :30-56, readLength :261-282
-        uint64_t rl = 0;
-        int st = uv(10, HONU_ERR_NO_LENGTH, rl);
-        if (st) return st;
-        if (rl >= (1ull << 63)) return HONU_ERR_PANIC;  // int(rl) < 0 -> makeslice
-        if (rl == 0) {
-            off = 0;
-            len = 0;
-            return HONU_OK;
-        }
-        if (rl > (uint64_t)INT64_MAX - (p - tstart)) return HONU_ERR_PANIC;  // d.i + rl overflows
-        if (p + rl > end) return HONU_ERR_UNEXPECTED_EOF;
-        off = p;
-        len = rl;
-        p += rl;
-        return HONU_OK;
-    }
-};
-
-// a step of the walk: runs only while the lane's record is still OK, so every
-// lane reaches the refill points (the wave stays converged there)
-#define STEP(x)                      \
-    do {                             \
-        if (st == HONU_OK) st = (x); \
-    } while (0)
-#define HONU_SKIP 0x7fffffff  // lane without a walk (past n, or header error)
-
-HONU_DEV void parse_win_one(
-    uint64_t i0, uint8_t *smem, const uint8_t *__restrict__ rec,
-    const uint64_t *__restrict__ rec_off, uint64_t n, honu_meta *__restrict__ meta,
-    honu_record_info *__restrict__ info, DecodeScratch *__restrict__ scratch,
-    uint32_t *__restrict__ reg_inline, uint64_t *__restrict__ counts) {
-    const uint32_t lane = lane_id();
-    const uint32_t wv = threadIdx.x / HONU_WAVE;
-    const uint64_t i = i0 + lane;
-    const bool valid = i < n;
-    LaneWin W;
-    W.wave = smem + wv * WIN_WAVE_BYTES;
-    W.wants = reinterpret_cast<uint64_t *>(W.wave + HONU_WAVE * WS);
-    W.rec = rec;
-    W.lim = rec_off[n];
-    W.wb = NOWIN;
-    W.lane = lane;
-
-    uint64_t beg = 0, end = 0;
-    if (valid) {
-        beg = rec_off[i];
-        end = rec_off[i + 1];
-    }
-    const uint64_t len = end - beg;
-    uint32_t ver = 0;
-    int64_t d = -1, b = -1;
-    if (valid && len) {
-        uint64_t lo, hi;
-        lane_fetch16(rec, beg, end, lo, hi);
-        ver = (uint32_t)(lo & 0xFF);
-        // dataLength (object.go:114-134): Uvarint(o[1 : min(11, len-1)])
-        if (len >= 3) {
-            const uint32_t wl = (uint32_t)(len - 2 < 10 ? len - 2 : 10);
-            const uint64_t lo1 = (lo >> 8) | (hi << 56), hi1 = hi >> 8;
-            uint64_t x;
-            const uint32_t k = uvarint_window(lo1, hi1, wl, x);
-            if (k) {
-                d = (int64_t)x;  // int(rl): negative for rl >= 2^63
-                b = k;
-            }
-        }
-    }
-    const bool v1 = ver == HONU_STORAGE_VERSION;
-    const bool in_range = d >= 0 && (uint64_t)d <= len - 1 - (uint64_t)b;
-    int32_t data_status;
-    uint64_t data_off = 0, data_len = 0;
-    if (!v1) data_status = HONU_ERR_BAD_VERSION;
-    else if (d < 0) data_status = HONU_ERR_MALFORMED;
-    else if (d == 0) data_status = HONU_OK;
-    else if (!in_range) data_status = HONU_ERR_PANIC;  // o[1+b:1+b+d]
-    else {
-        data_status = HONU_OK;
-        data_off = beg + 1 + (uint64_t)b;
-        data_len = (uint64_t)d;
-    }
-
-    Row R;
-    R.clear();
-    uint64_t nacl = 0, nreg = 0, acl_pos = 0, reg_pos = 0;
-    int st = HONU_OK;
-    if (!valid) st = HONU_SKIP;
-    else if (!v1) st = HONU_ERR_BAD_VERSION;
-    else if (d < 0) st = HONU_ERR_MALFORMED;
-    else if (!in_range) st = HONU_ERR_PANIC;  // o[1+d+b:]
-    WDec D;
-    D.w = &W;
-    D.end = end;
-    D.tstart = st == HONU_OK ? beg + 1 + (uint64_t)b + (uint64_t)d : 0;
-    D.p = D.tstart;
-    W.refill(st == HONU_OK ? (D.p & ~15ull) : NOWIN);
-
-    uint32_t f = 0, u = 0, pr = 0;
-    uint64_t v = 0, o = 0, l = 0, lo = 0, hi = 0;
-    int64_t t = 0;
-    STEP(D.boolean(f));                                     // DecodeStruct(meta) object.go:78
-    const bool hm = st == HONU_OK && f;
-    bool has_enc = false;
-    if (hm) {
-        pr = HONU_HAS_META;
-        STEP(D.ulid(lo, hi)); R.bytes16(OFF(object_id), lo, hi);       // metadata.go:210
-        STEP(D.ulid(lo, hi)); R.bytes16(OFF(collection_id), lo, hi);   // :214
-        STEP(D.boolean(f));                                 // :219 Version
-        if (st == HONU_OK && f) {
-            pr |= HONU_HAS_VERSION;
-            STEP(D.u32(u)); R.u32(OFF(pid), u);             // scalar.go:121-131
-            STEP(D.u64(v)); R.u64(OFF(vid), v);
-            STEP(D.u32(u)); R.u32(OFF(region), u);          // version.go:80
-            STEP(D.boolean(f));                             // :88 Parent
-            if (st == HONU_OK && f) {
-                pr |= HONU_HAS_PARENT;
-                STEP(D.u32(u)); R.u32(OFF(parent_pid), u);
-                STEP(D.u64(v)); R.u64(OFF(parent_vid), v);
-            }
-            STEP(D.boolean(f)); R.u8(OFF(tombstone), f);    // :96
-            STEP(D.i64(t)); R.u64(OFF(version_created), (uint64_t)t);  // :100
-        }
-        STEP(D.boolean(f));                                 // :225 Schema
-        if (st == HONU_OK && f) {
-            pr |= HONU_HAS_SCHEMA;
-            STEP(D.frame(o, l)); R.span(OFF(schema_name), o, l);       // schema.go:55-73
-            STEP(D.u32(u)); R.u32(OFF(schema_major), u);
-            STEP(D.u32(u)); R.u32(OFF(schema_minor), u);
-            STEP(D.u32(u)); R.u32(OFF(schema_patch), u);
-        }
-        STEP(D.frame(o, l)); R.span(OFF(mime), o, l);       // :231
-        STEP(D.ulid(lo, hi)); R.bytes16(OFF(owner), lo, hi);   // :235
-        STEP(D.ulid(lo, hi)); R.bytes16(OFF(group), lo, hi);   // :239
-        STEP(D.u8(u)); R.u8(OFF(permissions), u);           // :243
-        STEP(D.u64(nacl));                                  // :249
-        if (st == HONU_OK && nacl > GO_MAX_ALLOC / 8) st = HONU_ERR_PANIC;  // make([]*AccessControl)
-    }
-    // ACL entries (:254-265, acls.go:41-51): speculate every entry present
-    // (flags at p + 18 j) and check the flags window by window.
-    bool fast = false;
-    if (hm && st == HONU_OK && nacl > 0) {
-        acl_pos = D.p;
-        fast = 18 * nacl <= D.end - D.p;
-    }
-    {
-        bool chk = fast;
-        uint64_t ak = 0;
-        while (__ballot(chk)) {
-            W.refill(chk ? ((D.p + 18 * ak) & ~15ull) : NOWIN);
-            if (chk) {
-                uint64_t q = D.p + 18 * ak;
-                while (ak < nacl && q - W.wb < WB) {
-                    if (W.mine()[q - W.wb] != 1) {
-                        fast = false;
-                        break;
-                    }
-                    ak++;
-                    q += 18;
-                }
-                if (!fast || ak == nacl) chk = false;
-            }
-        }
-    }
-    if (hm && st == HONU_OK && nacl > 0) {
-        if (fast) {
-            D.p += 18 * nacl;
-            acl_pos |= GRP_ACL_FAST;  // for the group fill
-        } else {
-            for (uint64_t k = 0; k < nacl && st == HONU_OK; k++) {
-                STEP(D.boolean(f));
-                if (st == HONU_OK && f) {
-                    STEP(D.ulid(lo, hi));
-                    STEP(D.u8(u));
-                }
-            }
-        }
-        R.u64(OFF(acl_count), nacl);
-    }
-    W.refill(hm && st == HONU_OK ? (D.p & ~15ull) : NOWIN);
-    if (hm) {
-        STEP(D.u64(nreg));                                  // region.go:154-169
-        if (st == HONU_OK && nreg > GO_MAX_ALLOC / 4) st = HONU_ERR_PANIC;  // make(Regions, n)
-        pr |= HONU_REGIONS_NONNIL;
-        reg_pos = D.p;
-        for (uint64_t k = 0; k < nreg && st == HONU_OK; k++) {
-            STEP(D.u32(u));
-            if (st == HONU_OK && k < 8) reg_inline[8 * i + k] = u;
-        }
-        if (nreg <= 8) reg_pos |= GRP_REG_INLINE;
-        R.u64(OFF(regions_count), nreg);
-        STEP(D.boolean(f));                                 // :271 Publisher
-        if (st == HONU_OK && f) {
-            pr |= HONU_HAS_PUBLISHER;
-            STEP(D.ulid(lo, hi)); R.bytes16(OFF(publisher_id), lo, hi);   // provenance.go:59-79
-            STEP(D.ulid(lo, hi)); R.bytes16(OFF(client_id), lo, hi);
-            STEP(D.frame(o, l)); R.span(OFF(ip_address), o, l);
-            STEP(D.frame(o, l)); R.span(OFF(user_agent), o, l);
-        }
-        STEP(D.boolean(f));                                 // :277 Encryption
-        if (st == HONU_OK && f) {
-            pr |= HONU_HAS_ENCRYPTION;
-            has_enc = true;
-            STEP(D.frame(o, l)); R.span(OFF(public_key_id), o, l);     // encryption.go:91-125
-            STEP(D.frame(o, l)); R.span(OFF(encryption_key), o, l);
-            STEP(D.frame(o, l)); R.span(OFF(hmac_secret), o, l);
-            STEP(D.frame(o, l)); R.span(OFF(signature), o, l);
-        }
-    }
-    W.refill(hm && st == HONU_OK ? (D.p & ~15ull) : NOWIN);
-    if (hm) {
-        if (has_enc) {
-            STEP(D.u8(u)); R.u8(OFF(sealing_alg), u);
-            STEP(D.u8(u)); R.u8(OFF(encryption_alg), u);
-            STEP(D.u8(u)); R.u8(OFF(signature_alg), u);
-        }
-        STEP(D.boolean(f));                                 // :283 Compression
-        if (st == HONU_OK && f) {
-            pr |= HONU_HAS_COMPRESSION;
-            STEP(D.u8(u)); R.u8(OFF(compression_alg), u);   // compression.go:55-67
-            STEP(D.i64(t)); R.u64(OFF(compression_level), (uint64_t)t);
-        }
-        STEP(D.u8(u)); R.u8(OFF(flags), u);                 // :289
-        STEP(D.i64(t)); R.u64(OFF(created), (uint64_t)t);   // :293
-        STEP(D.i64(t)); R.u64(OFF(modified), (uint64_t)t);  // :297
-    }
-    R.u32(OFF(present), pr);
-    if (st != HONU_OK) {  // Go returns nil, err
-        R.clear();
-        nacl = nreg = 0;
-    }
-
-    // rows out through LDS: 32 rows per pass, written as contiguous 16-byte
-    // stores (the windows are free now)
-    for (uint32_t h = 0; h < 2; h++) {
-        wave_sync();
-        if ((lane >> 5) == h) {
-            u32x4 *dst = reinterpret_cast<u32x4 *>(W.wave + (lane & 31) * sizeof(honu_meta));
-#pragma unroll
-            for (int c = 0; c < 22; c++)
-                dst[c] = u32x4{R.d[4 * c], R.d[4 * c + 1], R.d[4 * c + 2], R.d[4 * c + 3]};
-        }
-        wave_sync();
-        const uint64_t r0 = i0 + 32 * h;
-        const uint64_t rows = r0 >= n ? 0 : (n - r0 < 32 ? n - r0 : 32);
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(W.wave);
-        u32x4 *out = reinterpret_cast<u32x4 *>(meta + r0);
-        for (uint32_t s = lane; s < rows * 22; s += HONU_WAVE) out[s] = src[s];
-    }
-    if (!valid) return;
-    honu_record_info inf;
-    inf.data_off = data_off;
-    inf.data_len = data_len;
-    inf.data_status = data_status;
-    inf.meta_status = st;
-    inf.storage_version = (uint8_t)ver;
-    inf.tombstone = (v1 && d == 0) ? 1 : 0;  // Tombstone :103-112
-#pragma unroll
-    for (int k = 0; k < 6; k++) inf._pad[k] = 0;
-    store_info(info + i, inf);
-    scratch[i] = DecodeScratch{acl_pos, reg_pos, data_off, end};
-    counts[3 * i + 0] = nacl;
-    counts[3 * i + 1] = nreg;
-    counts[3 * i + 2] = (data_len + 15) & ~15ull;
-}
-
-// one wave per 64 records, grid-stride over the batch (the loop is wave-uniform)
 __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_win(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
     honu_meta *__restrict__ meta, honu_record_info *__restrict__ info,
@@ -400,13 +13,27 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_win(
     uint64_t *__restrict__ counts) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * WIN_WAVE_BYTES];
     const uint32_t wv = threadIdx.x / HONU_WAVE;
+    uint8_t *ws = smem + wv * WIN_WAVE_BYTES;
+    // one wave per 64 records, grid-stride over the batch (the loop is wave-uniform)
     for (uint64_t i0 = (uint64_t)blockIdx.x * HONU_BLOCK + wv * HONU_WAVE; i0 < n;
-         i0 += (uint64_t)gridDim.x * HONU_BLOCK)
-        parse_win_one(i0, smem, rec, rec_off, n, meta, info, scratch, reg_inline, counts);
+         i0 += (uint64_t)gridDim.x * HONU_BLOCK) {
+        WinParse P;
+        win_walk(i0, ws, rec, rec_off, n, P);
+        rows_out(ws, P.R, i0, n, meta);
+        const uint64_t i = i0 + lane_id();
+        if (i >= n) continue;
+        store_info(info + i, make_info(P, P.data_off, P.data_len, P.data_status, P.st));
+        // the group fill takes inline regions from reg_inline (8 per record)
+        const uint64_t rp = P.nreg > 8 ? (P.reg_pos & GRP_POS_MASK) : P.reg_pos;
+        scratch[i] = DecodeScratch{P.acl_pos, rp, P.data_off, P.end};
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if ((uint64_t)k < P.nreg) reg_inline[8 * i + k] = P.regs[k];
+        counts[3 * i + 0] = P.nacl;
+        counts[3 * i + 1] = P.nreg;
+        counts[3 * i + 2] = (P.data_len + 15) & ~15ull;
+    }
 }
-
-#undef STEP
-#undef OFF
 
 static dim3 win_grid(uint64_t n, int cap) {
     const uint64_t b = (n + HONU_BLOCK - 1) / HONU_BLOCK;

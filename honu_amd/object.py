@@ -230,8 +230,18 @@ class Codec:
         self.scan(out_off, b.n, out_off)
         total = int(out_off.view(_torch().int64)[b.n].item())
         out = self._empty(total)
-        self.encode(b, out, total, out_off, status)
+        self.marshal_into(b, out, total, out_off, status)
         return EncodeResult(out, out_off, status, b.n)
+
+    def marshal_into(self, b: DeviceBatch, out, out_cap, out_off, status):
+        """honu_marshal_batch into a caller-sized arena: the single-launch
+        size/offset/header/tail kernel + the payload copy (record_variant 0),
+        or the split phases."""
+        _lib.check(self.lib.honu_marshal_batch(
+            self.ctx, _lib.ptr(b.meta), _lib.ptr(b.var), b.var_len, _lib.ptr(b.acl), b.acl_len,
+            _lib.ptr(b.regions), b.regions_len, _lib.ptr(b.payload), _lib.ptr(b.payload_off),
+            b.n, _lib.ptr(out), out_cap, _lib.ptr(out_off), _lib.ptr(status), self.stream),
+            "honu_marshal_batch")
 
     # ---- decode ---------------------------------------------------------
     def decode(self, rec, rec_off, n: int, materialize: bool = False,

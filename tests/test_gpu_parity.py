@@ -21,8 +21,8 @@ from honu_amd.metadata import META_DTYPE, normalize, pack_batch, unpack_row  # n
 from honu_amd.workload import gen_host_batch, gen_meta  # noqa: E402
 
 
-@pytest.fixture(scope="module", params=[0, 1, 2, 3, 4],
-                ids=["auto", "wave", "group", "lane", "lane+group"])
+@pytest.fixture(scope="module", params=[0, 5, 1, 2, 3, 4],
+                ids=["fused", "split", "wave", "group", "lane", "lane+group"])
 def codec(request):
     """Every metadata-kernel variant: auto (the default per-kernel choice: split
     lane/group encode, windowed lane parse), one record per wave, per group of
@@ -293,7 +293,7 @@ def test_long_tails_and_nil_entries_parity(codec, oracle_lib):
 
 
 @pytest.mark.parametrize("lens", ["tiny", "edges", "skew"])
-@pytest.mark.parametrize("copy_variant", [0, 1, 6, 11, 12], ids=["default", "unroll8", "sweep", "nt_load", "nt_store"])
+@pytest.mark.parametrize("copy_variant", [0, 1, 6, 11, 12, 13], ids=["default", "unroll8", "sweep", "nt_load", "nt_store", "unaligned"])
 def test_copy_engine_parity(oracle_lib, copy_variant, lens):
     """The payload copy engine on awkward length mixes: payloads of 0-40 bytes
     (head/tail bytes only), lengths around multiples of 16, and a skewed mix of
