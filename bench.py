@@ -78,6 +78,9 @@ def parse_args(argv=None):
     p.add_argument("--encode-copy-after", choices=["scan", "meta"], default="scan",
                    help="start a chunk's encode payload copy after its sizes + scan, or after "
                         "its header/tail encoder too")
+    p.add_argument("--decode", choices=["auto", "fused", "split"], default="auto",
+                   help="Metadata decode of a chunk: the single-launch kernel (fused), parse + "
+                        "tables (split), or by chunk size as honu_decode_batch (auto)")
     p.add_argument("--copy-blocks", type=int, default=0,
                    help="workgroups per CU of the payload copy engine (0 = library default)")
     return p.parse_args(argv)
@@ -257,12 +260,18 @@ class Bench:
         if self.args.encode_copy_after == "meta":
             ev_off = torch.cuda.Event()
             ev_off.record(sm)
-        _lib.check(L.honu_decode_parse(c, P(sl.out), P(sl.out_off), n, P(sl.dmeta),
-                                       P(sl.dinfo), ms), "decode_parse")
-        _lib.check(L.honu_decode_tables(c, P(sl.out), n, P(sl.dmeta), P(sl.dinfo),
-                                        P(sl.dacl), self.acl_cap, P(sl.dreg), self.reg_cap,
-                                        P(sl.data), self.data_cap, P(sl.totals), ms),
-                   "decode_tables")
+        if self.fused_decode(n):  # parse + look-back + tables in one launch (fused.hip)
+            _lib.check(L.honu_decode_records(c, P(sl.out), P(sl.out_off), n, P(sl.dmeta),
+                                             P(sl.dinfo), P(sl.dacl), self.acl_cap, P(sl.dreg),
+                                             self.reg_cap, 1, self.data_cap, P(sl.totals), ms),
+                       "decode_records")
+        else:
+            _lib.check(L.honu_decode_parse(c, P(sl.out), P(sl.out_off), n, P(sl.dmeta),
+                                           P(sl.dinfo), ms), "decode_parse")
+            _lib.check(L.honu_decode_tables(c, P(sl.out), n, P(sl.dmeta), P(sl.dinfo),
+                                            P(sl.dacl), self.acl_cap, P(sl.dreg), self.reg_cap,
+                                            P(sl.data), self.data_cap, P(sl.totals), ms),
+                       "decode_tables")
         ev_fill = torch.cuda.Event()
         ev_fill.record(sm)
         cs = sc.cuda_stream
@@ -290,6 +299,12 @@ class Bench:
         sl.free.record(sc)
         self.last = (a, b, sl)
         return sl
+
+    FUSED_DECODE_MIN = 128 << 10  # as honu_decode_batch: fused from 128 K records
+
+    def fused_decode(self, n):
+        d = self.args.decode
+        return d == "fused" or (d == "auto" and n >= self.FUSED_DECODE_MIN)
 
     def verify(self):
         """Every record of the batch, after the timed steps: one more pipelined
@@ -631,6 +646,7 @@ def main(argv=None):
             "meta_blocks_per_cu": 8 if (args.serial or not args.meta_blocks) else args.meta_blocks,
             "lane_blocks_per_cu": bench.lane_blocks or None,
             "copy_blocks_per_cu": args.copy_blocks or 2,
+            "metadata_decode": "fused" if bench.fused_decode(bench.C) else "split",
         },
         "records_per_s": total_records / step_s,
         "ranks": ranks,

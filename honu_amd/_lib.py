@@ -41,7 +41,6 @@ _PROTOS = {
     "honu_decode_tables": (I32, [P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),
     "honu_decode_payloads": (I32, [P, P, U64, P, P, P, P]),
     "honu_marshal_batch": (I32, [P, P, P, U64, P, U64, P, U64, P, P, U64, P, U64, P, P, P]),
-    "honu_marshal_records": (I32, [P, P, P, U64, P, U64, P, U64, P, U64, P, U64, P, P, P]),
     "honu_decode_parse": (I32, [P, P, P, U64, P, P, P]),
     "honu_decode_fill": (I32, [P, P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),
     "honu_decode_batch": (I32, [P, P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),

@@ -24,11 +24,11 @@ struct honu_ctx {
     DecodeScratch *scratch;  // max_n
     uint32_t *reg_inline;    // 8 * max_n: region ids handed from the group parse to fill
     uint64_t *enc_acl;       // max_n: ACL list positions, lane encoder -> group ACL encoder
-    // decoupled look-back state of the fused kernels (fused.hip): per kernel
-    // a ticket/epoch block and K status words per 64-record tile
-    LbState *lb_dec, *lb_enc;
-    uint64_t *lb_dec_status, *lb_enc_status;
-    uint64_t lb_dec_words, lb_enc_words;
+    // decoupled look-back state of the fused decode (fused.hip): a
+    // ticket/epoch block and 3 status words per 64-record tile
+    LbState *lb_dec;
+    uint64_t *lb_dec_status;
+    uint64_t lb_dec_words;
 };
 
 static thread_local char g_last_error[256];
@@ -51,8 +51,9 @@ static int32_t arg_fail(const char *what) {
 static bool aligned(const void *p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
 
 // record_variant 5 runs the batch entries through the split kernels of
-// variant 0 (the fused kernels are variant 0's batch path)
-static int split_rv(int rv) { return rv == 5 ? 0 : rv; }
+// variant 0, 6 through the fused decode at every size; variant 0 picks by size
+static int split_rv(int rv) { return rv == 5 || rv == 6 ? 0 : rv; }
+#define FUSED_DECODE_MIN_RECORDS (128ull << 10)
 
 // Fused kernels: persistent waves (2 workgroups of 4 waves per CU fit the LDS
 // and registers), fewer under a lane_blocks cap.
@@ -133,7 +134,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     const uint64_t np = scan_partials_len(n, 3) + scan_partials_len(n, 1);
     const uint64_t map_cap = 1ull << 22;  // tile map entries (sweep copy variants)
     const uint64_t tiles = (n + HONU_WAVE - 1) / HONU_WAVE;
-    const uint64_t lb_bytes = 2 * sizeof(LbState) + 8 * (3 * tiles + 1 * tiles);
+    const uint64_t lb_bytes = sizeof(LbState) + 8 * 3 * tiles;
     const uint64_t bytes = 8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 32 * n +
                            8 * n + 4 * map_cap + lb_bytes + 256;
     if (hipMalloc(&c->ws, bytes) != hipSuccess) {
@@ -158,11 +159,8 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->geom.tile_map = (uint32_t *)(c->enc_acl + n);
     c->geom.tile_map_cap = map_cap;
     c->lb_dec = (LbState *)(c->geom.tile_map + map_cap);
-    c->lb_enc = c->lb_dec + 1;
-    c->lb_dec_status = (uint64_t *)(c->lb_enc + 1);
+    c->lb_dec_status = (uint64_t *)(c->lb_dec + 1);
     c->lb_dec_words = 3 * tiles;
-    c->lb_enc_status = c->lb_dec_status + c->lb_dec_words;
-    c->lb_enc_words = tiles;
     // clean look-back state: epoch 0 with no published tile
     if (hipMemset(c->lb_dec, 0, lb_bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
         (void)hipFree(c->ws);
@@ -287,44 +285,12 @@ int32_t honu_encode(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var
                                 d_status, stream);
 }
 
-int32_t honu_marshal_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
-                             uint64_t var_len, const honu_acl *d_acl, uint64_t acl_len,
-                             const uint32_t *d_regions, uint64_t regions_len,
-                             const uint64_t *d_payload_off, uint64_t n, uint8_t *d_out,
-                             uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status,
-                             void *stream) {
-    if (!ctx) return arg_fail("ctx");
-    if (n > ctx->max_n) return HONU_E_WORKSPACE;
-    if (!d_out_off) return arg_fail("null pointer");
-    if (n && (!d_meta || !d_payload_off || !d_status)) return arg_fail("null pointer");
-    if (!aligned(d_meta, 16)) return arg_fail("rows must be 16-byte aligned");
-    if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
-    HIPCHK(hipSetDevice(ctx->device));
-    hipStream_t s = (hipStream_t)stream;
-    if (n == 0) {
-        HIPCHK(hipMemsetAsync(d_out_off, 0, sizeof(uint64_t), s));
-        return HONU_OK;
-    }
-    HIPCHK(launch_encode_fused(d_meta, d_var, var_len, d_acl, acl_len, d_regions, regions_len,
-                               d_payload_off, n, d_out, out_cap, d_out_off, d_status, ctx->lb_enc,
-                               ctx->lb_enc_status, ctx->lb_enc_words, fused_blocks(ctx->geom), s));
-    return HONU_OK;
-}
-
 int32_t honu_marshal_batch(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
                            uint64_t var_len, const honu_acl *d_acl, uint64_t acl_len,
                            const uint32_t *d_regions, uint64_t regions_len,
                            const uint8_t *d_payload, const uint64_t *d_payload_off, uint64_t n,
                            uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off,
                            int32_t *d_status, void *stream) {
-    if (ctx && ctx->geom.record_variant == 0) {  // fused (default)
-        int32_t st = honu_marshal_records(ctx, d_meta, d_var, var_len, d_acl, acl_len, d_regions,
-                                          regions_len, d_payload_off, n, d_out, out_cap, d_out_off,
-                                          d_status, stream);
-        if (st) return st;
-        return honu_encode_payloads(ctx, d_payload, d_payload_off, n, d_out, out_cap, d_out_off,
-                                    d_status, stream);
-    }
     int32_t st = honu_encode_sizes(ctx, d_meta, var_len, d_acl, acl_len, d_regions, regions_len,
                                    d_payload_off, n, d_out_off, d_status, stream);
     if (st) return st;
@@ -451,7 +417,11 @@ int32_t honu_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
                           honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
                           uint64_t regions_cap, uint8_t *d_data, uint64_t data_cap,
                           uint64_t *d_totals, void *stream) {
-    if (ctx && ctx->geom.record_variant == 0) {  // fused (default)
+    // fused for batches of more than one round of resident waves (measured
+    // faster from ~128 K records; below, the split kernels' extra waves hide
+    // the walk's latency better), always with record_variant 6
+    const int rv = ctx ? ctx->geom.record_variant : 0;
+    if (rv == 6 || (rv == 0 && n >= FUSED_DECODE_MIN_RECORDS)) {
         if (d_data && !aligned(d_data, 16)) return arg_fail("data arena must be 16-byte aligned");
         int32_t st = honu_decode_records(ctx, d_rec, d_rec_off, n, d_meta, d_info, d_acl, acl_cap,
                                          d_regions, regions_cap, d_data != nullptr, data_cap,

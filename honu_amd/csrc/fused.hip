@@ -1,16 +1,15 @@
-// fused.hip — single-launch Metadata decode (honu_decode_records /
-// honu_decode_batch) and single-launch header + Metadata encode
-// (honu_marshal_records / honu_marshal_batch).
+// fused.hip — single-launch Metadata decode (honu_decode_records, and
+// honu_decode_batch for large batches).
 //
-// The split pipelines (win.hip + scan.hip + grp.hip; grp.hip + scan.hip +
-// lane.hip) hand per-record counts, positions and offsets between five to
-// seven launches through the context scratch, and each later launch reads the
-// rows / ACL bytes again. Here one wave owns a tile of 64 consecutive
-// records (one per lane) from the first byte to the last: the wave walks or
-// sizes its records, the decoupled look-back (lookback.h) turns the counts
-// into table / output offsets, and the wave writes every output with those
-// offsets — rows and row fields once, ACL bytes re-read right after the walk
-// fetched them (L2-resident), no scratch round trips, no launch boundaries.
+// The split decode (win.hip + scan.hip + grp.hip) hands per-record counts,
+// positions and inline region ids between five launches through the context
+// scratch; the fill re-reads the ACL bytes from HBM and patches the rows. Here
+// one wave owns a tile of 64 consecutive records (one per lane) from the first
+// byte to the last: the wave walks its records (win.h), the decoupled
+// look-back (lookback.h) turns the counts into table offsets, and the wave
+// writes every output with those offsets — rows once, region ids from
+// registers, ACL entries re-read right after the walk — with no scratch round
+// trips and no launch boundaries.
 #include <stdlib.h>
 
 #include "lookback.h"
@@ -233,168 +232,6 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
     return hipGetLastError();
 }
 
-
-// ------------------------------------------------------------------------
-// encode: object.Marshal (object.go:24-45) of every record except the payload
-// bytes: exact size, output offset (look-back), header + Metadata tail
-// (metadata.go:108-200). One column: the encoded bytes.
-// ------------------------------------------------------------------------
-#ifndef ENC_COUNT_U
-#define ENC_COUNT_U 16
-#endif
-#ifndef ENC_CHUNK_U
-#define ENC_CHUNK_U 4
-#endif
-constexpr uint32_t EROW = 368;                  // LDS stride of a staged row (92 dwords:
-                                                // the lanes of a ds_read_b128 hit distinct banks)
-constexpr uint32_t ESTAGE = 32 * EROW;          // half a tile of rows
-struct EncodeIn {
-    const honu_meta *meta;
-    const uint8_t *var;
-    uint64_t var_len;
-    const honu_acl *acl;
-    uint64_t acl_len;
-    const uint32_t *reg;
-    uint64_t reg_len;
-    const uint64_t *payload_off;
-};
-
-__global__ __launch_bounds__(HONU_BLOCK, 2) void k_encode_fused(
-    EncodeIn I, uint64_t n, uint8_t *__restrict__ out, uint64_t out_cap,
-    uint64_t *__restrict__ out_off, int32_t *__restrict__ status, LbState *lb,
-    uint64_t *lb_status, uint64_t lb_words) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * ESTAGE];
-    uint8_t *ws = smem + (threadIdx.x / HONU_WAVE) * ESTAGE;
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(ws);  // 64 counters, after the rows are read
-    const uint32_t lane = lane_id();
-    const uint32_t ep = lb_epoch(lb);
-    const uint64_t ntiles = (n + HONU_WAVE - 1) / HONU_WAVE;
-    uint64_t t;
-    for (;;) {
-        t = lb_ticket(lb);
-        if (t >= ntiles) break;
-        const uint64_t i0 = t * HONU_WAVE, i = i0 + lane;
-        const bool valid = i < n;
-        // the tile's rows: coalesced 16-byte loads -> LDS -> one row per lane
-        honu_meta m;
-        for (uint32_t h = 0; h < 2; h++) {
-            const uint64_t r0 = i0 + 32 * h;
-            const uint32_t rows = r0 >= n ? 0 : (uint32_t)(n - r0 < 32 ? n - r0 : 32);
-            const u32x4 *src = reinterpret_cast<const u32x4 *>(I.meta + r0);
-            wave_sync();
-            for (uint32_t s = lane; s < rows * 22; s += HONU_WAVE)
-                *reinterpret_cast<u32x4 *>(ws + (s / 22) * EROW + (s % 22) * 16) = src[s];
-            wave_sync();
-            if ((lane >> 5) == h) {
-                const u32x4 *row = reinterpret_cast<const u32x4 *>(ws + (lane & 31) * EROW);
-                u32x4 *dst = reinterpret_cast<u32x4 *>(&m);
-#pragma unroll
-                for (int c = 0; c < 22; c++) dst[c] = row[c];
-            }
-        }
-        wave_sync();
-        int32_t st = valid ? encode_check(m, I.var_len, I.acl_len, I.reg_len) : HONU_SKIP;
-        const uint64_t tail = st == HONU_OK ? encode_tail_bytes_noacl(m, I.reg) : 0;
-        // present ACL entries per record: the wave's lists as one run of
-        // entries (record by a search over the prefixes), counted in LDS
-        const uint64_t na = st == HONU_OK ? m.acl_count : 0, ao = m.acl_off;
-        uint64_t atot;
-        const uint64_t apre = wave_excl(na, atot);
-        cnt[lane] = 0;
-        wave_sync();
-        constexpr int UC = ENC_COUNT_U;  // entries per lane in flight
-        for (uint64_t e0 = 0; e0 < atot; e0 += UC * HONU_WAVE) {  // wave-uniform
-            uint32_t pz[UC], rr[UC];
-#pragma unroll
-            for (int k = 0; k < UC; k++) {
-                const uint64_t e = e0 + lane + HONU_WAVE * k;
-                const uint32_t r = lane_search(apre, e < atot ? e : 0);
-                rr[k] = r;
-                const uint64_t src = shfl64(ao, r) + (e - shfl64(apre, r));
-                pz[k] = e < atot ? I.acl[src].present : 0;
-            }
-#pragma unroll
-            for (int k = 0; k < UC; k++)
-                if (pz[k]) atomicAdd(&cnt[rr[k]], 1u);
-        }
-        wave_sync();
-        const uint64_t present = cnt[lane];
-        const uint64_t dlen = valid ? I.payload_off[i + 1] - I.payload_off[i] : 0;
-        const uint64_t size = st == HONU_OK ? 1 + uvarint_len(dlen) + dlen + tail + na + 17 * present : 0;
-
-        // sizes -> output offsets: wave scan + look-back across tiles
-        uint64_t agg[1], excl[1];
-        const uint64_t x = wave_excl(size, agg[0]);
-        lb_scan<1>(lb_status, t, ep, agg, excl);
-        const uint64_t beg = excl[0] + x, end = beg + size;
-        if (t == ntiles - 1 && lane == 0) out_off[n] = excl[0] + agg[0];
-        if (st == HONU_OK && end > out_cap) st = HONU_ERR_CAPACITY;
-        if (valid) {
-            out_off[i] = beg;
-            status[i] = st;
-        }
-
-        // header + tail but the ACL entries (the lane), then the entries
-        uint64_t pos = 0;
-        if (st == HONU_OK) pos = encode_record_lane<true>(m, I.var, I.acl, I.reg, dlen, beg, end, out);
-        const bool all = st == HONU_OK && na && (pos & ACL_ALL_PRESENT);
-        const uint64_t P = pos & ~ACL_ALL_PRESENT;
-        if (st == HONU_OK && na && !all) {  // nil entries: 00, else 01 | ClientID | Permissions
-            uint64_t p = P;
-            for (uint64_t j = 0; j < na; j++) {
-                const honu_acl *a = I.acl + ao + j;
-                if (a->present) {
-                    uint32_t d[5];
-                    acl_enc_words(a, d);
-                    for (int b = 0; b < 18; b++) out[p + b] = (uint8_t)(d[b >> 2] >> (8 * (b & 3)));
-                    p += 18;
-                } else {
-                    out[p++] = 0;
-                }
-            }
-        }
-        // every entry present: the whole aligned 16-byte chunks of the lists
-        // [ceil16(P), floor16(P + 18 na)) as one run of chunks over the wave
-        const uint64_t X0 = (P + 15) & ~15ull, X1 = (P + 18 * na) & ~15ull;
-        const uint64_t nch = all && X1 > X0 ? (X1 - X0) >> 4 : 0;
-        uint64_t ctot;
-        const uint64_t cpre = wave_excl(nch, ctot);
-        constexpr int UK = ENC_CHUNK_U;  // chunks per lane in flight
-        for (uint64_t c0 = 0; c0 < ctot; c0 += UK * HONU_WAVE) {  // wave-uniform
-            u32x4 v[UK];
-            uint64_t dst[UK];
-#pragma unroll
-            for (int k = 0; k < UK; k++) {
-                const uint64_t c = c0 + lane + HONU_WAVE * k;
-                const uint32_t r = lane_search(cpre, c < ctot ? c : 0);
-                const uint64_t rP = shfl64(P, r), rX0 = shfl64(X0, r), rna = shfl64(na, r),
-                               rao = shfl64(ao, r);
-                dst[k] = rX0 + 16 * (c - shfl64(cpre, r));
-                if (c < ctot) v[k] = acl_chunk(I.acl + rao, rna, rP, dst[k]);
-            }
-#pragma unroll
-            for (int k = 0; k < UK; k++)
-                if (c0 + lane + HONU_WAVE * k < ctot) *reinterpret_cast<u32x4 *>(out + dst[k]) = v[k];
-        }
-    }
-    lb_finish(lb, lb_status, lb_words, t, ntiles, gridDim.x * HONU_WAVES_PER_BLOCK);
-}
-
-hipError_t launch_encode_fused(const honu_meta *meta, const uint8_t *var, uint64_t var_len,
-                               const honu_acl *acl, uint64_t acl_len, const uint32_t *reg,
-                               uint64_t reg_len, const uint64_t *payload_off, uint64_t n,
-                               uint8_t *out, uint64_t out_cap, uint64_t *out_off, int32_t *status,
-                               LbState *lb, uint64_t *lb_status, uint64_t lb_words,
-                               int max_blocks, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    const uint64_t tiles = (n + HONU_WAVE - 1) / HONU_WAVE;
-    uint64_t b = (tiles + HONU_WAVES_PER_BLOCK - 1) / HONU_WAVES_PER_BLOCK;
-    if (max_blocks > 0 && b > (uint64_t)max_blocks) b = (uint64_t)max_blocks;
-    EncodeIn I{meta, var, var_len, acl, acl_len, reg, reg_len, payload_off};
-    hipLaunchKernelGGL(k_encode_fused, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, I, n, out,
-                       out_cap, out_off, status, lb, lb_status, lb_words);
-    return hipGetLastError();
-}
 
 #undef OFF
 

@@ -176,13 +176,6 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
                                uint64_t *totals, LbState *lb, uint64_t *lb_status,
                                uint64_t lb_words, int max_blocks, hipStream_t s);
 
-hipError_t launch_encode_fused(const honu_meta *meta, const uint8_t *var, uint64_t var_len,
-                               const honu_acl *acl, uint64_t acl_len, const uint32_t *reg,
-                               uint64_t reg_len, const uint64_t *payload_off, uint64_t n,
-                               uint8_t *out, uint64_t out_cap, uint64_t *out_off, int32_t *status,
-                               LbState *lb, uint64_t *lb_status, uint64_t lb_words,
-                               int max_blocks, hipStream_t s);
-
 hipError_t launch_decode_parse_win(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                    honu_meta *meta, honu_record_info *info,
                                    DecodeScratch *scratch, uint32_t *reg_inline, uint64_t *counts,

@@ -192,11 +192,12 @@ uint64_t honu_ctx_max_records(const honu_ctx *ctx);
  * "lane_blocks" (cap on workgroups of the lane, group and window kernels;
  * default 0 = no cap — a cap leaves room for a concurrent payload copy),
  * "copy_variant" (copy-engine variant, default 0), "record_variant" (how the
- * per-record metadata kernels map records to lanes: 0 auto — the fused
- * single-launch kernels for the batch entries and the fastest measured form
- * per kernel for the split entries, 5 the split kernels for the batch entries
- * too; A/B builds add 1 one record per wave, 2 one record per group of 16
- * lanes, 3 one record per lane, 4 lane walks with group lists). Also
+ * per-record metadata kernels map records to lanes: 0 auto — the fastest
+ * measured form per kernel, with honu_decode_batch running the single-launch
+ * decode for batches of 128 K records or more; 5 the split decode at every
+ * size; 6 the single-launch decode at every size; A/B builds add 1 one record
+ * per wave, 2 one record per group of 16 lanes, 3 one record per lane, 4 lane
+ * walks with group lists). Also
  * settable at context creation through the environment (HONU_COPY_BLOCKS,
  * HONU_RECORD_BLOCKS, HONU_LANE_BLOCKS, HONU_COPY_VARIANT, HONU_RECORD_VARIANT). */
 int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value);
@@ -262,22 +263,7 @@ int32_t honu_encode_payloads(honu_ctx *ctx, const uint8_t *d_payload, const uint
                              uint64_t n, uint8_t *d_out, uint64_t out_cap,
                              const uint64_t *d_out_off, const int32_t *d_status, void *stream);
 
-/* Sizes + offsets + headers and Metadata tails in ONE launch (the default
- * batch encode): d_out_off (n+1) and d_status as honu_encode_sizes +
- * honu_exclusive_scan produce them (HONU_ERR_CAPACITY as honu_encode_records
- * sets it), and every record's bytes but the payload, which
- * honu_encode_payloads (any stream, after this call) copies. Rows are read
- * once; the output is identical to the split path's. */
-int32_t honu_marshal_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
-                             uint64_t var_len, const honu_acl *d_acl, uint64_t acl_len,
-                             const uint32_t *d_regions, uint64_t regions_len,
-                             const uint64_t *d_payload_off, uint64_t n, uint8_t *d_out,
-                             uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status,
-                             void *stream);
-
-/* sizes + scan + encode in one call; d_out_off (n+1) is produced here:
- * honu_marshal_records + honu_encode_payloads (record_variant 5: the split
- * phases). */
+/* sizes + scan + encode in one call; d_out_off (n+1) is produced here. */
 int32_t honu_marshal_batch(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
                            uint64_t var_len, const honu_acl *d_acl, uint64_t acl_len,
                            const uint32_t *d_regions, uint64_t regions_len,
@@ -333,8 +319,8 @@ int32_t honu_decode_records(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t 
                             uint64_t regions_cap, int32_t materialize, uint64_t data_cap,
                             uint64_t *d_totals, void *stream);
 
-/* parse + fill in one call: honu_decode_records (+ honu_decode_payloads when
- * d_data != NULL); record_variant 5 runs the split phases instead. */
+/* parse + fill in one call: from 128 K records honu_decode_records (+
+ * honu_decode_payloads when d_data != NULL), below the split phases. */
 int32_t honu_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
                           uint64_t n, honu_meta *d_meta, honu_record_info *d_info,
                           honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,

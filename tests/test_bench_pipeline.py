@@ -6,7 +6,8 @@ tables run on one stream while the payload copies run on a second stream, the
 encode copy starting after the scan so it writes payload bytes into the same
 16-byte chunks the header/tail encoder is writing around them; two output
 slots alternate across chunks and across steps. Here Bench itself runs that
-pipeline on small batches split into 5 chunks for 2 steps, and every chunk of
+pipeline on small batches split into 5 chunks for 2 steps (with the
+single-launch decode and with the split parse + tables), and every chunk of
 every step is compared with oracle.marshal_batch / oracle.decode_batch once it
 has drained (while the next chunk runs): encoded bytes, offsets, statuses,
 full 352-byte rows, record info, ACL and region tables and every materialised
@@ -34,12 +35,14 @@ def _gpu():
         pytest.skip("no GPU")
 
 
+@pytest.mark.parametrize("decode", ["fused", "split"])
 @pytest.mark.parametrize("after", ["scan", "meta"])
 @pytest.mark.parametrize("shape,n", [("small", 4000), ("mixed", 1200), ("large", 160)])
-def test_bench_pipeline_bit_exact(oracle_lib, shape, n, after):
+def test_bench_pipeline_bit_exact(oracle_lib, shape, n, after, decode):
     seed = 7
     args = bench.parse_args(["--records", str(n), "--shape", shape, "--min-chunks", "5",
-                             "--encode-copy-after", after, "--seed", str(seed)])
+                             "--encode-copy-after", after, "--seed", str(seed),
+                             "--decode", decode])
     b = bench.Bench(args, 0, 0)
     assert len(b.chunks) >= 5 and len(b.slots) == 2
     hb = gen_host_batch(seed, shape, 0, n)  # the same records the device generator made

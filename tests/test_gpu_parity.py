@@ -21,12 +21,15 @@ from honu_amd.metadata import META_DTYPE, normalize, pack_batch, unpack_row  # n
 from honu_amd.workload import gen_host_batch, gen_meta  # noqa: E402
 
 
-@pytest.fixture(scope="module", params=[0, 5, 1, 2, 3, 4],
+@pytest.fixture(scope="module", params=[6, 5, 1, 2, 3, 4],
                 ids=["fused", "split", "wave", "group", "lane", "lane+group"])
 def codec(request):
-    """Every metadata-kernel variant: auto (the default per-kernel choice: split
-    lane/group encode, windowed lane parse), one record per wave, per group of
-    16 lanes, per lane, and lane encode/parse with the group size pass/fill."""
+    """Every metadata-kernel variant: the single-launch decode (fused.hip) at
+    every batch size, the split kernels of the default path (group size pass,
+    lane encode with group ACL lists, windowed lane parse, group fill), one
+    record per wave, per group of 16 lanes, per lane, and lane encode/parse
+    with the group size pass/fill. (The default picks fused or split by batch
+    size; the bench pipeline tests and the large-batch tests run it.)"""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     c = hobj.Codec(0, 1 << 18)

@@ -85,10 +85,6 @@ def main():
                 "fused_mat": lambda: L.honu_decode_records(c, P(out), P(out_off), n, P(dmeta),
                                                            P(dinfo), P(dacl), acl_cap, P(dreg),
                                                            reg_cap, 1, data.numel(), P(tot), s),
-                # single-launch encode of sizes, offsets, headers and tails
-                "fused_enc": lambda: L.honu_marshal_records(c, P(dm), P(dv), len(var), P(da), len(acl),
-                                                            P(dr), len(reg), P(do), n, P(out), cap,
-                                                            P(out_off), P(st), s),
             }
             times = {k: [] for k in stages}
             for r in range(a.reps + 1):
