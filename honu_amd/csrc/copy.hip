@@ -129,6 +129,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t 
     }
 }
 
+#ifdef HONU_AB
 // ------------------------------------------------------------------------
 // Sweep form: the logical space is cut into tiles of T bytes and wave w
 // copies tiles w, w+W, w+2W, ... so that at any moment all waves work inside
@@ -187,14 +188,19 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_sweep(Seg seg, uint64_t n,
     }
 }
 
-// Copy-engine variants: 0-5 contiguous per-wave ranges {unroll, non-temporal};
-// 6-7 the sweep form; 11 / 12 non-temporal loads only / stores only. Variant 0 is the default; the others exist for the
-// measurement sweeps in tools/tune_copy.py.
+#endif  // HONU_AB
+
+// Copy-engine variants (A/B build only, tools/tune_copy.py): 1-5 contiguous
+// per-wave ranges {unroll, non-temporal}; 6-7 the sweep form; 11 / 12
+// non-temporal loads only / stores only; 13-15 one unaligned 16-byte load per
+// chunk instead of two aligned loads and a funnel. The product library has
+// variant 0 only (unroll 4, default cache policy: measured fastest).
 template <class Seg>
 static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
                               const uint64_t *total, hipStream_t s) {
     const dim3 grid(g.copy_blocks * SMALL_SEG_WAVES_FACTOR), block(HONU_BLOCK);
-    if (g.copy_variant >= 6) {
+#ifdef HONU_AB
+    if (g.copy_variant >= 6 && g.copy_variant <= 7) {
         if (!g.tile_map) return hipErrorInvalidValue;
         hipLaunchKernelGGL((k_tile_map<Seg>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                            seg, n, total, g.tile_map, g.tile_map_cap);
@@ -205,18 +211,20 @@ static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
         return hipGetLastError();
     }
     switch (g.copy_variant) {
-    case 1: hipLaunchKernelGGL((k_copy_segments<Seg, 8, 0>), grid, block, 0, s, seg, n, total); break;
-    case 2: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 1>), grid, block, 0, s, seg, n, total); break;
-    case 3: hipLaunchKernelGGL((k_copy_segments<Seg, 8, 1>), grid, block, 0, s, seg, n, total); break;
-    case 4: hipLaunchKernelGGL((k_copy_segments<Seg, 2, 0>), grid, block, 0, s, seg, n, total); break;
-    case 5: hipLaunchKernelGGL((k_copy_segments<Seg, 16, 0>), grid, block, 0, s, seg, n, total); break;
-    case 11: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 2>), grid, block, 0, s, seg, n, total); break;
-    case 12: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 3>), grid, block, 0, s, seg, n, total); break;
-    case 13: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 4>), grid, block, 0, s, seg, n, total); break;
-    case 14: hipLaunchKernelGGL((k_copy_segments<Seg, 8, 4>), grid, block, 0, s, seg, n, total); break;
-    case 15: hipLaunchKernelGGL((k_copy_segments<Seg, 2, 4>), grid, block, 0, s, seg, n, total); break;
-    default: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0>), grid, block, 0, s, seg, n, total); break;
+    case 1: hipLaunchKernelGGL((k_copy_segments<Seg, 8, 0>), grid, block, 0, s, seg, n, total); return hipGetLastError();
+    case 2: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 1>), grid, block, 0, s, seg, n, total); return hipGetLastError();
+    case 3: hipLaunchKernelGGL((k_copy_segments<Seg, 8, 1>), grid, block, 0, s, seg, n, total); return hipGetLastError();
+    case 4: hipLaunchKernelGGL((k_copy_segments<Seg, 2, 0>), grid, block, 0, s, seg, n, total); return hipGetLastError();
+    case 5: hipLaunchKernelGGL((k_copy_segments<Seg, 16, 0>), grid, block, 0, s, seg, n, total); return hipGetLastError();
+    case 11: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 2>), grid, block, 0, s, seg, n, total); return hipGetLastError();
+    case 12: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 3>), grid, block, 0, s, seg, n, total); return hipGetLastError();
+    case 13: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 4>), grid, block, 0, s, seg, n, total); return hipGetLastError();
+    case 14: hipLaunchKernelGGL((k_copy_segments<Seg, 8, 4>), grid, block, 0, s, seg, n, total); return hipGetLastError();
+    case 15: hipLaunchKernelGGL((k_copy_segments<Seg, 2, 4>), grid, block, 0, s, seg, n, total); return hipGetLastError();
+    default: break;
     }
+#endif
+    hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0>), grid, block, 0, s, seg, n, total);
     return hipGetLastError();
 }
 

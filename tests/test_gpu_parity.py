@@ -25,15 +25,19 @@ from honu_amd.workload import gen_host_batch, gen_meta  # noqa: E402
                 ids=["fused", "split", "wave", "group", "lane", "lane+group"])
 def codec(request):
     """Every metadata-kernel variant: the single-launch decode (fused.hip) at
-    every batch size, the split kernels of the default path (group size pass,
-    lane encode with group ACL lists, windowed lane parse, group fill), one
-    record per wave, per group of 16 lanes, per lane, and lane encode/parse
-    with the group size pass/fill. (The default picks fused or split by batch
-    size; the bench pipeline tests and the large-batch tests run it.)"""
+    every batch size, and the split kernels of the default path (group size
+    pass, lane encode with group ACL lists, windowed lane parse, group fill).
+    The A/B library (make ab; HONU_LIB_PATH=honu_amd/libhonu_codec_ab.so)
+    adds one record per wave, per group of 16 lanes, per lane, and lane
+    encode/parse with the group size pass/fill; the product library refuses
+    those variants and they are skipped. (The default picks fused or split by
+    batch size; the bench pipeline and large-batch tests run it.)"""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     c = hobj.Codec(0, 1 << 18)
-    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", request.param), "param")
+    if c.lib.honu_ctx_set_param(c.ctx, b"record_variant", request.param) != 0:
+        c.close()
+        pytest.skip("A/B kernel variant: not in the product library")
     yield c
     c.close()
 
@@ -323,7 +327,8 @@ def test_copy_engine_parity(oracle_lib, copy_variant, lens):
     hb = HostBatch(base.meta, base.var, base.acl, base.regions, pay, off)
     c = hobj.Codec(0, n)
     try:
-        hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"copy_variant", copy_variant), "param")
+        if c.lib.honu_ctx_set_param(c.ctx, b"copy_variant", copy_variant) != 0:
+            pytest.skip("A/B copy variant: not in the product library")
         out, goff, st = gpu_marshal(c, hb)
         oout, ooff, ost = oracle_lib.marshal_batch(hb)
         assert np.array_equal(st, ost) and np.array_equal(goff, ooff)
