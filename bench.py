@@ -614,10 +614,10 @@ def main(argv=None):
     traffic, traffic_src = None, None
     tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tpath):  # PMC passes of this same command (tools/pmc_traffic.py)
-        pm = json.load(open(tpath))
+        pm = json.load(open(tpath)).get("workloads", {}).get(workload, {})
         kn = dom_name.split("<")[0] + "<" + dom_name.split("<")[1].split(">")[0]
         for k, v in pm.get("kernels", {}).items():
-            if pm.get("workload") == workload and k.startswith("void honu::" + kn):
+            if k.startswith("void honu::" + kn):
                 traffic, traffic_src = v["traffic_per_launch"], "profiles/pmc_traffic.json"
     result = {
         "metric": METRIC,

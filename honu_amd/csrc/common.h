@@ -73,6 +73,36 @@ HONU_DEV uint32_t wave_inclusive_scan32(uint32_t v) {
 }
 HONU_DEV uint64_t wave_sum(uint64_t v) { return readlane64(wave_inclusive_scan(v), 63); }
 
+// Wave exclusive scan of v (64-bit); *total = the wave's sum.
+HONU_DEV uint64_t wave_excl(uint64_t v, uint64_t &total) {
+    const uint64_t inc = wave_inclusive_scan(v);
+    total = readlane64(inc, 63);
+    return inc - v;
+}
+
+// Largest lane r with pre(r) <= e, for pre non-decreasing over the lanes
+// (each lane its own e; pre read with ds_bpermute).
+HONU_DEV uint32_t lane_search(uint64_t pre, uint64_t e) {
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1) {
+        const uint32_t mid = lo + step;
+        const uint64_t v = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(pre >> 32), (int)mid) << 32) |
+                           (uint32_t)__shfl((int)(uint32_t)pre, (int)mid);
+        if (mid < 64 && v <= e) lo = mid;
+    }
+    return lo;
+}
+HONU_DEV uint64_t shfl_xor64(uint64_t v, int d) {
+    return ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), d) << 32) |
+           (uint32_t)__shfl_xor((int)(uint32_t)v, d);
+}
+HONU_DEV uint64_t shfl64(uint64_t v, uint32_t src) {
+    return ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src) << 32) |
+           (uint32_t)__shfl((int)(uint32_t)v, (int)src);
+}
+
+
 // ------------------------------------------------------------------------
 // lani / encoding/binary varint arithmetic
 // ------------------------------------------------------------------------

@@ -179,6 +179,22 @@ struct WDec {  // lani.Decoder (lani/decode.go) over [tstart, end), as LaneDec
 
 #define HONU_SKIP 0x7fffffff  // lane without a walk (past n)
 
+// Timing build only (-DHONU_WALK_TIMING, tools/walk_timing.py): lane 0 of every
+// wave records s_memrealtime (100 MHz) at fixed points of its first walk.
+#ifdef HONU_WALK_TIMING
+#define WALK_STAMPS 10
+static __device__ uint64_t g_walk_stamps[1 << 16][WALK_STAMPS];  // per translation unit
+#define WSTAMP(k)                                                                          \
+    do {                                                                                   \
+        const uint64_t wid_ = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + threadIdx.x / 64; \
+        if (lane_id() == 0 && wid_ < (1 << 16)) g_walk_stamps[wid_][k] = wall_clock64();      \
+    } while (0)
+#else
+#define WSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
+
 // What the walk of one record leaves in the lane's registers.
 struct WinParse {
     Row R;              // the decoded row (acl_off / regions_off not yet set)
@@ -208,12 +224,14 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
     const uint32_t lane = lane_id();
     const uint64_t i = i0 + lane;
     const bool valid = i < n;
+    WSTAMP(0);  // walk entered
     uint64_t beg = 0, end = 0;
     if (valid) {
         beg = rec_off[i];
         end = rec_off[i + 1];
     }
     LaneWin W;
+    WSTAMP(1);  // rec_off loaded
     W.init(wave_smem, rec, end);
     const uint64_t len = end - beg;
     uint32_t ver = 0;
@@ -266,7 +284,9 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
     D.end = end;
     D.tstart = st == HONU_OK ? beg + 1 + (uint64_t)b + (uint64_t)d : 0;
     D.p = D.tstart;
+    WSTAMP(2);  // header read
     W.refill(st == HONU_OK ? (D.p & ~15ull) : NOWIN);
+    WSTAMP(3);  // first window
 
     uint32_t f = 0, u = 0, pr = 0;
     uint64_t v = 0, o = 0, l = 0, lo = 0, hi = 0;
@@ -306,6 +326,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
         STEP(D.ulid(lo, hi)); R.bytes16(OFF(group), lo, hi);   // :239
         STEP(D.u8(u)); R.u8(OFF(permissions), u);           // :243
         STEP(D.u64(nacl));                                  // :249
+        WSTAMP(4);  // fields up to the ACL count
         if (st == HONU_OK && nacl > GO_MAX_ALLOC / 8) st = HONU_ERR_PANIC;  // make([]*AccessControl)
     }
     // ACL entries (:254-265, acls.go:41-51): speculate every entry present
@@ -352,7 +373,9 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
         }
         R.u64(OFF(acl_count), nacl);
     }
+    WSTAMP(5);  // ACL flags checked
     W.refill(hm && st == HONU_OK ? (D.p & ~15ull) : NOWIN);
+    WSTAMP(6);  // window after the list
     if (hm) {
         STEP(D.u64(nreg));                                  // region.go:154-169
         if (st == HONU_OK && nreg > GO_MAX_ALLOC / 4) st = HONU_ERR_PANIC;  // make(Regions, n)
@@ -386,7 +409,9 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
             STEP(D.frame(o, l)); R.span(OFF(signature), o, l);
         }
     }
+    WSTAMP(7);  // regions .. signature
     W.refill(hm && st == HONU_OK ? (D.p & ~15ull) : NOWIN);
+    WSTAMP(8);  // window after the signature
     if (hm) {
         if (has_enc) {
             STEP(D.u8(u)); R.u8(OFF(sealing_alg), u);
@@ -408,6 +433,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
         R.clear();
         nacl = nreg = 0;
     }
+    WSTAMP(9);  // walk done
     P.st = st;
     P.nacl = nacl;
     P.nreg = nreg;

@@ -6,6 +6,16 @@
 
 namespace honu {
 
+#ifdef HONU_WALK_TIMING
+}  // namespace honu
+extern "C" int32_t honu_debug_walk_stamps(void *host, uint64_t waves) {
+    if (waves > (1 << 16)) waves = 1 << 16;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(honu::g_walk_stamps),
+                               waves * WALK_STAMPS * sizeof(uint64_t)) == hipSuccess ? 0 : -3;
+}
+namespace honu {
+#endif
+
 __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_win(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
     honu_meta *__restrict__ meta, honu_record_info *__restrict__ info,

@@ -7,7 +7,11 @@ coalesced streaming read (16 B per lane), so it is doubled; WRITE_SIZE is exact
 for 16-B-per-lane streaming stores.
 
 usage: pmc_traffic.py FETCH_CSV WRITE_CSV WORKLOAD OUT_JSON
+OUT_JSON holds one entry per workload ({"workloads": {WORKLOAD: ...}}); an
+existing file is updated in place, so the bench lines of several commands
+share it (bench.py reads the entry of its own workload).
 """
+import os
 import collections
 import csv
 import json
@@ -35,7 +39,12 @@ def main():
         wb = 1024 * sum(wv) / max(1, len(wv))
         res["kernels"][k] = {"launches": max(len(fv), len(wv)), "read_bytes_per_launch": fb,
                              "write_bytes_per_launch": wb, "traffic_per_launch": fb + wb}
-    json.dump(res, open(out, "w"), indent=1)
+    allw = {"workloads": {}}
+    if os.path.exists(out):
+        old = json.load(open(out))
+        allw["workloads"] = old.get("workloads", {})
+    allw["workloads"][workload] = res
+    json.dump(allw, open(out, "w"), indent=1)
     for k, v in res["kernels"].items():
         print(f"{k[:60]:60s} {v['traffic_per_launch'] / 1e9:10.3f} GB/launch")
 
