@@ -36,7 +36,8 @@ struct DecodeOut {
     DecodeScratch *scratch;   // materialize: payload sources for honu_decode_payloads
     uint64_t *offs;           // materialize: offs[3i+2] = data arena offset
     uint64_t *totals;         // column totals (3)
-    int dbg;                  // measurement knobs (HONU_FUSED_DBG): 1 no ACL fill, 2 no look-back wait
+    int dbg;                  // A/B measurement knobs (HONU_FUSED_DBG): 1 no ACL fill,
+                              // 2 no look-back wait, 4 static tiles (with 2)
 };
 
 __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
@@ -200,7 +201,11 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
     const uint64_t tiles = (n + HONU_WAVE - 1) / HONU_WAVE;
     uint64_t b = (tiles + HONU_WAVES_PER_BLOCK - 1) / HONU_WAVES_PER_BLOCK;
     if (max_blocks > 0 && b > (uint64_t)max_blocks) b = (uint64_t)max_blocks;
+#ifdef HONU_AB  // measurement knobs, A/B library only (they break the results)
     static const int dbg = getenv("HONU_FUSED_DBG") ? atoi(getenv("HONU_FUSED_DBG")) : 0;
+#else
+    const int dbg = 0;
+#endif
     DecodeOut O{meta, info, acl, acl_cap, reg, reg_cap, data_cap, materialize, scratch, offs, totals, dbg};
     hipLaunchKernelGGL(k_decode_fused, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
                        O, lb, lb_status, lb_words);

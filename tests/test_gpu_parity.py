@@ -462,11 +462,14 @@ def test_decode_parse_full_waves(codec, oracle_lib):
     assert acl.tobytes() == oacl.tobytes() and reg.tobytes() == oreg.tobytes()
 
 
-def test_hip_graph_capture_replay(oracle_lib):
+@pytest.mark.parametrize("rv", [0, 6], ids=["split", "fused"])
+def test_hip_graph_capture_replay(oracle_lib, rv):
     """The ABI's calls neither allocate nor synchronise (include/honu_codec.h),
     so a whole marshal + decode + keys sequence is captured into one hipGraph
     (torch.cuda.CUDAGraph over the capturing stream) and replayed: outputs are
-    recomputed from the device inputs at every replay, bit-exact."""
+    recomputed from the device inputs at every replay, bit-exact. With the
+    single-launch decode the look-back's epoch lives in device memory, so
+    replays of the same launch arguments stay correct."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     L = hobj._lib
@@ -475,6 +478,7 @@ def test_hip_graph_capture_replay(oracle_lib):
     oout, ooff, _ = oracle_lib.marshal_batch(hb)
     ometa, oinfo, oacl, oreg, odata, otot = oracle_lib.decode_batch(oout, ooff, True)
     c = hobj.Codec(0, n)
+    L.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", rv), "param")
     try:
         db = hobj.DeviceBatch.from_host(hb, c.torch_device)
         total = int(ooff[-1])

@@ -1,0 +1,88 @@
+"""The single-launch decode's cross-tile scan (honu_amd/csrc/lookback.h) over
+many launches: status words carry an 18-bit launch epoch kept in device memory
+and are never cleared between launches, except when the epoch wraps. A wide
+batch (many tiles) publishes words for every tile; 2^18 - 1 one-tile launches
+then advance the epoch to its wrap, where the status array must be cleared: a
+second wide batch with different counts decodes bit-exact only if no stale
+word of the first one is taken for its own. Also: batches of 1..300 tiles in
+a row, each checked against the oracle (every look-back window size)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from honu_amd import object as hobj  # noqa: E402
+from honu_amd.workload import gen_host_batch  # noqa: E402
+
+EPOCHS = 1 << 18
+
+
+def _dev(a, codec):
+    return hobj._dev_bytes(np.ascontiguousarray(a), codec.torch_device)
+
+
+class _Dec:
+    """Preallocated honu_decode_records over one encoded batch."""
+
+    def __init__(self, codec, rec, off):
+        self.c, self.n = codec, len(off) - 1
+        self.rec, self.off = _dev(rec, codec), _dev(off, codec)
+        cap = int(off[-1])
+        self.acl_cap = self.reg_cap = cap
+        e = codec._empty
+        self.meta, self.info, self.tot = e(352 * self.n), e(32 * self.n), e(32)
+        self.acl, self.reg = e(20 * cap), e(4 * cap)
+
+    def __call__(self):
+        L = hobj._lib
+        return self.c.lib.honu_decode_records(
+            self.c.ctx, L.ptr(self.rec), L.ptr(self.off), self.n, L.ptr(self.meta),
+            L.ptr(self.info), L.ptr(self.acl), self.acl_cap, L.ptr(self.reg), self.reg_cap, 0, 0,
+            L.ptr(self.tot), self.c.stream)
+
+    def check(self, oracle_lib, rec, off):
+        torch.cuda.synchronize()
+        ometa, oinfo, oacl, oreg, _, otot = oracle_lib.decode_batch(rec, off, False)
+        tot = self.tot[:24].cpu().numpy().view(np.uint64)
+        assert np.array_equal(tot, otot)
+        assert self.meta[:352 * self.n].cpu().numpy().tobytes() == ometa.tobytes()
+        assert self.info[:32 * self.n].cpu().numpy().tobytes() == oinfo.tobytes()
+        assert self.acl[:20 * int(otot[0])].cpu().numpy().tobytes() == oacl.tobytes()
+        assert self.reg[:4 * int(otot[1])].cpu().numpy().tobytes() == oreg.tobytes()
+
+
+@pytest.fixture(scope="module")
+def codec():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    c = hobj.Codec(0, 64 * 400)
+    yield c
+    c.close()
+
+
+def test_tile_counts(codec, oracle_lib):
+    for tiles, seed in ((1, 1), (2, 2), (3, 3), (65, 4), (66, 5), (129, 6), (300, 7)):
+        n = 64 * tiles - (seed % 3) * 7  # ragged last tile too
+        rec, off, _ = oracle_lib.marshal_batch(gen_host_batch(seed, "small", 0, n))
+        d = _Dec(codec, rec, off)
+        assert d() == 0
+        d.check(oracle_lib, rec, off)
+
+
+def test_epoch_wrap_clears_stale_words(codec, oracle_lib):
+    wide1 = oracle_lib.marshal_batch(gen_host_batch(11, "small", 0, 64 * 200))
+    wide2 = oracle_lib.marshal_batch(gen_host_batch(12, "small", 0, 64 * 200))
+    tiny = oracle_lib.marshal_batch(gen_host_batch(13, "small", 0, 64))
+    d1, d2, dt = _Dec(codec, *wide1[:2]), _Dec(codec, *wide2[:2]), _Dec(codec, *tiny[:2])
+    # wherever the context's epoch stands, bring it to EPOCHS - 1 launches
+    # before a wrap: one wide launch, then tiny ones up to the wrap
+    assert d1() == 0
+    d1.check(oracle_lib, *wide1[:2])
+    for _ in range(EPOCHS - 1):
+        assert dt() == 0
+    # the epoch has wrapped (or is past it) exactly once since d1's words
+    assert d2() == 0
+    d2.check(oracle_lib, *wide2[:2])
+    dt.check(oracle_lib, *tiny[:2])
