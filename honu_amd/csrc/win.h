@@ -345,15 +345,16 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
             if (!first) W.refill(chk ? ((D.p + 18 * ak) & ~15ull) : NOWIN);
             first = false;
             if (chk) {
-                uint64_t q = D.p + 18 * ak;
-                while (ak < nacl && W.in(q)) {
-                    if (W.at(q) != 1) {
-                        fast = false;
-                        break;
-                    }
-                    ak++;
-                    q += 18;
-                }
+                // the flags this window holds (at most 15), read independently
+                const uint64_t q = D.p + 18 * ak;
+                const uint64_t room = W.in(q) ? (W.wb + WB - q + 17) / 18 : 0;
+                const uint32_t cnt = (uint32_t)(nacl - ak < room ? nacl - ak : room);
+                bool ok = true;
+#pragma unroll
+                for (uint32_t j = 0; j < (WB + 17) / 18; j++)
+                    if (j < cnt) ok &= W.at(q + 18 * j) == 1;
+                ak += cnt;
+                if (!ok) fast = false;  // the entries are walked one by one below
                 if (!fast || ak == nacl) chk = false;
             }
         }
