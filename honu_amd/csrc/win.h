@@ -330,20 +330,51 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
         if (st == HONU_OK && nacl > GO_MAX_ALLOC / 8) st = HONU_ERR_PANIC;  // make([]*AccessControl)
     }
     // ACL entries (:254-265, acls.go:41-51): speculate every entry present
-    // (flags at p + 18 j) and check the flags window by window.
+    // (flags at p + 18 j). The first 64 flags of every lane's list are
+    // gathered in ONE round trip: the windows' LDS is free at this point (the
+    // walk is past every byte it holds), and instruction k of a 64-instruction
+    // burst of dword global_load_lds has lane j fetch flag j of lane k's list
+    // (one list per instruction: 64 flags 18 bytes apart, a few cache lines);
+    // every lane then checks its own flags with independent LDS reads. Flags
+    // past the 64th are checked window by window.
     bool fast = false;
     if (hm && st == HONU_OK && nacl > 0) {
         acl_pos = D.p;
         fast = 18 * nacl <= D.end - D.p;
     }
+    uint64_t ak = 0;
+    if (__ballot(fast)) {
+        const uint64_t gbase = fast ? acl_pos : 0;
+        const uint32_t gcnt = fast ? (uint32_t)(nacl < 64 ? nacl : 64) : 0;
+        wave_sync();  // the windows' last reads are done
+#pragma unroll 4
+        for (uint32_t k = 0; k < HONU_WAVE; k++) {
+            const uint64_t base = readlane64(gbase, k);  // lane k's list, to every lane
+            if (lane < __builtin_amdgcn_readlane(gcnt, k))
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(rec + ((base + 18ull * lane) & ~3ull)),
+                    (__attribute__((address_space(3))) void *)(W.wave + 256 * k), 4, 0, 0);
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        wave_sync();
+        W.wb = NOWIN;  // the windows' bytes are gone
+        if (fast) {
+            const uint32_t m = (uint32_t)(nacl < 64 ? nacl : 64);
+            const __attribute__((address_space(3))) uint8_t *fl =
+                (const __attribute__((address_space(3))) uint8_t *)(W.wave + 256 * lane);
+            bool ok = true;
+#pragma unroll
+            for (uint32_t j = 0; j < 64; j++)
+                if (j < m) ok &= fl[4 * j + (uint32_t)((acl_pos + 18ull * j) & 3)] == 1;
+            ak = m;
+            if (!ok) fast = false;  // the entries are walked one by one below
+        }
+        wave_sync();  // the gather area becomes windows again
+    }
     {
-        bool chk = fast;
-        uint64_t ak = 0;
-        bool first = true;
+        bool chk = fast && ak < nacl;
         while (__ballot(chk)) {
-            // the first round checks the flags the current window already holds
-            if (!first) W.refill(chk ? ((D.p + 18 * ak) & ~15ull) : NOWIN);
-            first = false;
+            W.refill(chk ? ((D.p + 18 * ak) & ~15ull) : NOWIN);
             if (chk) {
                 // the flags this window holds (at most 15), read independently
                 const uint64_t q = D.p + 18 * ak;
