@@ -20,7 +20,6 @@ struct honu_ctx {
     uint64_t *counts;        // 3 * max_n
     uint64_t *offs;          // 3 * max_n
     uint64_t *totals;        // 4
-    uint64_t *partials;      // scan partials
     DecodeScratch *scratch;  // max_n
     uint32_t *reg_inline;    // 8 * max_n: region ids handed from the group parse to fill
     uint64_t *enc_acl;       // max_n: ACL list positions, lane encoder -> group ACL encoder
@@ -29,6 +28,7 @@ struct honu_ctx {
     LbState *lb_dec;
     uint64_t *lb_dec_status;
     uint64_t lb_dec_words;
+    ScanState scan;          // look-back state of the one-launch scans (scan.hip)
 };
 
 static thread_local char g_last_error[256];
@@ -139,10 +139,11 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     if (!HONU_AB_BUILD && c->geom.record_variant != 5 && c->geom.record_variant != 6)
         c->geom.record_variant = 0;
     const uint64_t n = c->max_n;
-    const uint64_t np = scan_partials_len(n, 3) + scan_partials_len(n, 1);
+    const uint64_t np = 0;
     const uint64_t map_cap = HONU_AB_BUILD ? 1ull << 22 : 0;  // tile map (A/B sweep copy)
     const uint64_t tiles = (n + HONU_WAVE - 1) / HONU_WAVE;
-    const uint64_t lb_bytes = sizeof(LbState) + 8 * 3 * tiles;
+    const uint64_t scan_words = scan_status_words(n);
+    const uint64_t lb_bytes = 2 * sizeof(LbState) + 8 * (3 * tiles + scan_words);
     const uint64_t bytes = 8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 32 * n +
                            8 * n + 4 * map_cap + lb_bytes + 256;
     if (hipMalloc(&c->ws, bytes) != hipSuccess) {
@@ -159,16 +160,18 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     w += 3 * n;
     c->totals = w;
     w += 4;
-    c->partials = w;
-    w += np;
     c->scratch = (DecodeScratch *)w;
     c->reg_inline = (uint32_t *)(c->scratch + n);
     c->enc_acl = (uint64_t *)(c->reg_inline + 8 * n);
     c->geom.tile_map = (uint32_t *)(c->enc_acl + n);
     c->geom.tile_map_cap = map_cap;
     c->lb_dec = (LbState *)(c->geom.tile_map + map_cap);
-    c->lb_dec_status = (uint64_t *)(c->lb_dec + 1);
+    c->scan.lb = c->lb_dec + 1;
+    c->lb_dec_status = (uint64_t *)(c->scan.lb + 1);
     c->lb_dec_words = 3 * tiles;
+    c->scan.status = c->lb_dec_status + c->lb_dec_words;
+    c->scan.words = scan_words;
+    c->scan.max_blocks = 4 * prop.multiProcessorCount;
     // clean look-back state: epoch 0 with no published tile
     if (hipMemset(c->lb_dec, 0, lb_bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
         (void)hipFree(c->ws);
@@ -240,7 +243,7 @@ int32_t honu_exclusive_scan(honu_ctx *ctx, const uint64_t *d_in, uint64_t n, uin
     if (!ctx) return arg_fail("ctx");
     if (n > ctx->max_n) return HONU_E_WORKSPACE;
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(launch_scan(d_in, n, 1, d_out, d_out + n, ctx->partials, (hipStream_t)stream));
+    HIPCHK(launch_scan(d_in, n, 1, d_out, d_out + n, ctx->scan, (hipStream_t)stream));
     return HONU_OK;
 }
 
@@ -378,7 +381,7 @@ int32_t honu_decode_tables(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n, honu
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     uint64_t *tot = d_totals ? d_totals : ctx->totals;
-    HIPCHK(launch_scan(ctx->counts, n, 3, ctx->offs, tot, ctx->partials, s));
+    HIPCHK(launch_scan(ctx->counts, n, 3, ctx->offs, tot, ctx->scan, s));
     const int rv = split_rv(ctx->geom.record_variant);
 #ifdef HONU_AB
     if (rv == 3) {
@@ -501,7 +504,7 @@ int32_t honu_decode_data_place(honu_ctx *ctx, const uint8_t *d_rec, const uint64
     }
     // spans -> exclusive scan of the aligned sizes (offs[n] = total) -> place
     HIPCHK(launch_decode_spans(d_rec, d_rec_off, n, d_info, ctx->scratch, ctx->counts, s));
-    HIPCHK(launch_scan(ctx->counts, n, 1, ctx->offs, ctx->offs + n, ctx->partials, s));
+    HIPCHK(launch_scan(ctx->counts, n, 1, ctx->offs, ctx->offs + n, ctx->scan, s));
     HIPCHK(launch_decode_data_place(n, d_info, ctx->offs, data_cap, s));
     if (d_totals)
         HIPCHK(hipMemcpyAsync(d_totals, ctx->offs + n, 8, hipMemcpyDeviceToDevice, s));
@@ -604,7 +607,7 @@ static int32_t collection_decode(honu_ctx *ctx, bool headless, const uint8_t *d_
     uint64_t *tot = d_totals ? d_totals : ctx->totals;
     HIPCHK(launch_system_parse(d_rec, d_rec_off, n, headless, d_rows, d_status, ctx->scratch,
                                ctx->counts, s));
-    HIPCHK(launch_scan(ctx->counts, n, 3, ctx->offs, tot, ctx->partials, s));
+    HIPCHK(launch_scan(ctx->counts, n, 3, ctx->offs, tot, ctx->scan, s));
     HIPCHK(launch_system_fill(d_rec, n, d_rows, d_status, ctx->scratch, ctx->counts, ctx->offs,
                               d_acl, acl_cap, d_regions, regions_cap, d_index, index_cap, s));
     return HONU_OK;

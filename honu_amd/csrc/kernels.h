@@ -210,10 +210,17 @@ hipError_t launch_span_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t n,
                             const uint64_t *offs, uint8_t *data, hipStream_t s);
 
 // Exclusive scan of K interleaved u64 columns: out[i*K+c] = sum_{j<i} in[j*K+c];
-// totals[c] = full sum. `partials` needs scan_partials_len(n, K) u64.
-uint64_t scan_partials_len(uint64_t n, int K);
+// totals[c] = full sum. One launch (decoupled look-back over tiles); the
+// state is the context's (scan_status_words(n) status words).
+struct ScanState {
+    LbState *lb;
+    uint64_t *status;
+    uint64_t words;
+    int max_blocks;
+};
+uint64_t scan_status_words(uint64_t n);
 hipError_t launch_scan(const uint64_t *in, uint64_t n, int K, uint64_t *out, uint64_t *totals,
-                       uint64_t *partials, hipStream_t s);
+                       const ScanState &S, hipStream_t s);
 
 hipError_t launch_gen_payload(const LaunchGeom &g, uint64_t seed, uint64_t first, uint64_t n,
                               const uint64_t *payload_off, uint8_t *payload, hipStream_t s);

@@ -32,111 +32,88 @@ HONU_DEV uint64_t block_incl_scan(uint64_t v, uint64_t *sh, uint64_t *total) {
     return incl + add;
 }
 
+// One launch: tiles of HONU_BLOCK * ITEMS rows taken in order by an atomic
+// ticket (one per workgroup); a tile sums its rows, wave 0 turns the tile's
+// column sums into its exclusive prefixes with the decoupled look-back
+// (lookback.h) and the workgroup writes its rows. in may alias out.
 template <int K>
-__global__ __launch_bounds__(HONU_BLOCK) void k_scan_reduce(const uint64_t *__restrict__ in,
-                                                            uint64_t n,
-                                                            uint64_t *__restrict__ partials) {
+__global__ __launch_bounds__(HONU_BLOCK) void k_scan_lb(const uint64_t *in, uint64_t n, uint64_t *out,
+                                                        uint64_t *__restrict__ totals, ScanState S) {
     constexpr int ITEMS = ScanCfg<K>::ITEMS;
     __shared__ uint64_t sh[HONU_WAVES_PER_BLOCK];
-    const uint64_t base = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) * ITEMS;
-    uint64_t s[K];
+    __shared__ uint64_t pre[K];
+    __shared__ uint32_t tile_sh;
+    const uint32_t ep = lb_epoch(S.lb);
+    const uint64_t rows = (uint64_t)HONU_BLOCK * ITEMS;
+    const uint64_t ntiles = (n + rows - 1) / rows;
+    uint64_t t;
+    for (;;) {
+        if (threadIdx.x == 0)
+            tile_sh = __hip_atomic_fetch_add(&S.lb->ticket, 1u, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        t = tile_sh;
+        if (t >= ntiles) break;
+        const uint64_t base = (t * HONU_BLOCK + threadIdx.x) * ITEMS;
+        uint64_t v[ITEMS][K], s[K], x[K], agg[K];
 #pragma unroll
-    for (int c = 0; c < K; c++) s[c] = 0;
-#pragma unroll
-    for (int it = 0; it < ITEMS; it++) {
-        const uint64_t row = base + it;
-        if (row < n) {
-#pragma unroll
-            for (int c = 0; c < K; c++) s[c] += in[row * K + c];
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < K; c++) {
-        uint64_t tot;
-        block_incl_scan(s[c], sh, &tot);
-        if (threadIdx.x == 0) partials[(uint64_t)blockIdx.x * K + c] = tot;
-    }
-}
-
-// One block: exclusive scan of the nb tile sums in place; totals[c] = sum.
-template <int K>
-__global__ __launch_bounds__(HONU_BLOCK) void k_scan_top(uint64_t *__restrict__ partials,
-                                                         uint64_t nb,
-                                                         uint64_t *__restrict__ totals) {
-    __shared__ uint64_t sh[HONU_WAVES_PER_BLOCK];
-    const uint64_t per = (nb + HONU_BLOCK - 1) / HONU_BLOCK;
-    const uint64_t j0 = threadIdx.x * per;
-    const uint64_t j1 = j0 + per < nb ? j0 + per : nb;
-    for (int c = 0; c < K; c++) {
-        uint64_t local = 0;
-        for (uint64_t j = j0; j < j1; j++) local += partials[j * K + c];
-        uint64_t tot;
-        const uint64_t incl = block_incl_scan(local, sh, &tot);
-        uint64_t run = incl - local;
-        for (uint64_t j = j0; j < j1; j++) {
-            const uint64_t v = partials[j * K + c];
-            partials[j * K + c] = run;
-            run += v;
-        }
-        if (threadIdx.x == 0) totals[c] = tot;
-    }
-}
-
-template <int K>
-__global__ __launch_bounds__(HONU_BLOCK) void k_scan_apply(const uint64_t *in, uint64_t n,
-                                                           const uint64_t *__restrict__ partials,
-                                                           uint64_t *out) {
-    constexpr int ITEMS = ScanCfg<K>::ITEMS;
-    __shared__ uint64_t sh[HONU_WAVES_PER_BLOCK];
-    const uint64_t base = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) * ITEMS;
-    uint64_t v[ITEMS][K];
-    uint64_t s[K];
-#pragma unroll
-    for (int c = 0; c < K; c++) s[c] = 0;
-#pragma unroll
-    for (int it = 0; it < ITEMS; it++) {
-        const uint64_t row = base + it;
-#pragma unroll
-        for (int c = 0; c < K; c++) {
-            v[it][c] = row < n ? in[row * K + c] : 0;
-            s[c] += v[it][c];
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < K; c++) {
-        uint64_t tot;
-        const uint64_t incl = block_incl_scan(s[c], sh, &tot);
-        uint64_t run = incl - s[c] + partials[(uint64_t)blockIdx.x * K + c];
+        for (int c = 0; c < K; c++) s[c] = 0;
 #pragma unroll
         for (int it = 0; it < ITEMS; it++) {
             const uint64_t row = base + it;
-            if (row < n) out[row * K + c] = run;
-            run += v[it][c];
+#pragma unroll
+            for (int c = 0; c < K; c++) {
+                v[it][c] = row < n ? in[row * K + c] : 0;
+                s[c] += v[it][c];
+            }
         }
+#pragma unroll
+        for (int c = 0; c < K; c++) x[c] = block_incl_scan(s[c], sh, &agg[c]) - s[c];
+        if (threadIdx.x < HONU_WAVE) {  // wave 0: the tile's prefix across tiles
+            uint64_t excl[K];
+            lb_scan<K>(S.status, t, ep, agg, excl);
+#pragma unroll
+            for (int c = 0; c < K; c++) {
+                if (threadIdx.x == 0) pre[c] = excl[c];
+                if (threadIdx.x == 0 && t == ntiles - 1) totals[c] = excl[c] + agg[c];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < K; c++) {
+            uint64_t run = pre[c] + x[c];
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++) {
+                const uint64_t row = base + it;
+                if (row < n) out[row * K + c] = run;
+                run += v[it][c];
+            }
+        }
+        __syncthreads();  // pre and tile_sh are rewritten by the next tile
     }
+    if (threadIdx.x < HONU_WAVE) lb_finish(S.lb, S.status, S.words, t, ntiles, gridDim.x);
 }
 
-uint64_t scan_partials_len(uint64_t n, int K) {
-    const uint64_t tile = (uint64_t)HONU_BLOCK * (K == 1 ? ScanCfg<1>::ITEMS : ScanCfg<3>::ITEMS);
-    return ((n + tile - 1) / tile + 1) * (uint64_t)K;
+uint64_t scan_status_words(uint64_t n) {  // the most K * tiles of any column count
+    const uint64_t t3 = (n + HONU_BLOCK * ScanCfg<3>::ITEMS - 1) / (HONU_BLOCK * ScanCfg<3>::ITEMS);
+    const uint64_t t1 = (n + HONU_BLOCK * ScanCfg<1>::ITEMS - 1) / (HONU_BLOCK * ScanCfg<1>::ITEMS);
+    return 3 * t3 > t1 ? 3 * t3 + 3 : t1 + 3;
 }
 
 template <int K>
 static hipError_t scan_k(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *totals,
-                         uint64_t *partials, hipStream_t s) {
-    const uint64_t tile = (uint64_t)HONU_BLOCK * ScanCfg<K>::ITEMS;
-    const uint64_t nb = (n + tile - 1) / tile;
-    hipLaunchKernelGGL(k_scan_reduce<K>, dim3((unsigned)nb), dim3(HONU_BLOCK), 0, s, in, n, partials);
-    hipLaunchKernelGGL(k_scan_top<K>, dim3(1), dim3(HONU_BLOCK), 0, s, partials, nb, totals);
-    hipLaunchKernelGGL(k_scan_apply<K>, dim3((unsigned)nb), dim3(HONU_BLOCK), 0, s, in, n, partials, out);
+                         const ScanState &S, hipStream_t s) {
+    const uint64_t tiles = (n + HONU_BLOCK * ScanCfg<K>::ITEMS - 1) / (HONU_BLOCK * ScanCfg<K>::ITEMS);
+    const uint64_t b = tiles < (uint64_t)S.max_blocks ? tiles : (uint64_t)S.max_blocks;
+    hipLaunchKernelGGL(k_scan_lb<K>, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, in, n, out, totals, S);
     return hipGetLastError();
 }
 
 hipError_t launch_scan(const uint64_t *in, uint64_t n, int K, uint64_t *out, uint64_t *totals,
-                       uint64_t *partials, hipStream_t s) {
+                       const ScanState &S, hipStream_t s) {
     if (n == 0) return hipMemsetAsync(totals, 0, sizeof(uint64_t) * K, s);
-    if (K == 1) return scan_k<1>(in, n, out, totals, partials, s);
-    if (K == 3) return scan_k<3>(in, n, out, totals, partials, s);
+    if (K == 1) return scan_k<1>(in, n, out, totals, S, s);
+    if (K == 3) return scan_k<3>(in, n, out, totals, S, s);
     return hipErrorInvalidValue;
 }
 
