@@ -1,26 +1,15 @@
-// grp.hip — the per-record metadata kernels with one record per GROUP of G
-// lanes (record_variant 2; the size pass and the fill also in variant 0).
+// grp.hip — the list kernels of the default path with one record per GROUP
+// of 16 lanes: the encode size pass, the encoder's ACL entries and the split
+// decode's table fill (the group walk and group encoder of record_variant 2
+// are A/B-only: ab/grp_walk.hip).
 //
-// Why groups: with one record per lane (lane.hip) each load instruction
-// touches 64 different cache lines, one per record, and a CU's 32 KiB L1
-// cannot keep the lines of all resident waves from one field to the next, so
-// L2 serves every field again (measured at 1M Small: decode parse 0.69 ns,
-// decode fill 1.37 ns, encode 1.24 ns per record — 2-6x the HBM time of the
-// bytes those kernels move). With one record per wave (encode.hip/decode.hip)
-// the serial lani walk is issued once per record for 64 lanes. Here G lanes
-// share one record:
-//   * the record's bytes move between HBM and LDS once, as aligned 16-byte
-//     accesses spread over the group (row image, Metadata tail);
-//   * the serial lani walk runs on LDS with every lane of the group in
-//     lockstep — the lanes agree on every position, nothing is broadcast;
-//   * the lists (ACL entries, regions) and the frame bytes are spread over the
-//     group's lanes, positions from group ballots and prefix sums;
-//   * the encoder builds the tail in a zeroed LDS stage with OR writes (every
-//     byte has exactly one writer, so order does not matter) and leaves it as
-//     aligned 16-byte stores; bytes it does not own (payload, neighbours) are
-//     never written.
-// Tails longer than the stage are built in several windows (encode) or walked
-// straight from global memory (decode) by the same code.
+// Why groups for lists: with one record per lane each load instruction
+// touches 64 different cache lines, one per record; with 16 lanes per record
+// the entries of a record's ACL list (20-byte rows in, 18-byte encodings out)
+// and its regions spread over the group's lanes, so loads and stores of one
+// instruction cover a few contiguous lines, and positions come from group
+// ballots and prefix sums. The row image is staged in LDS by the group as
+// aligned 16-byte loads.
 #include "grp.h"
 
 namespace honu {

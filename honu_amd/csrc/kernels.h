@@ -85,11 +85,11 @@ struct LaunchGeom {
     int copy_blocks;        // blocks of the byte-balanced copy kernel
     int copy_variant;       // copy engine variant (copy.hip: unroll depth / cache policy)
     int record_variant;     // per-record kernels: 0 auto (the fastest measured form
-                            // of each: group size pass, lane encode with the ACL
-                            // lists by groups, windowed lane parse, group fill),
-                            // 1 one record per wave, 2 one record per group of 16
-                            // lanes (grp.hip), 3 one record per lane (lane.hip),
-                            // 4 group size pass and fill, lane encode and parse
+                            // of each; honu_decode_batch single-launch from 128 K
+                            // records), 5 split decode, 6 single-launch decode
+                            // at every size; A/B library only: 1 one record per
+                            // wave, 2 per group of 16 lanes, 3 per lane, 4 group
+                            // size pass and fill with lane encode and parse
     uint32_t *tile_map;     // sweep-form tile -> segment map (context scratch)
     uint64_t tile_map_cap;
 };
