@@ -69,10 +69,14 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         const uint64_t x0 = wave_excl(c0, agg[0]);
         const uint64_t x1 = wave_excl(c1, agg[1]);
         const uint64_t x2 = wave_excl(c2, agg[2]);
+        // publish, then write the rows while the predecessors finish (their
+        // list offsets are patched in below), then wait
+        if (!(O.dbg & 2)) lb_publish<3>(lb_status, t, ep, agg);
+        rows_out(ws, P.R, i0, n, O.meta);
         if (O.dbg & 2) {
             excl[0] = excl[1] = excl[2] = 0;
         } else {
-            lb_scan<3>(lb_status, t, ep, agg, excl);
+            lb_resolve<3>(lb_status, t, ep, agg, excl);
         }
         if (t == ntiles - 1 && lane < 3)
             O.totals[lane] = lane == 0 ? excl[0] + agg[0] : (lane == 1 ? excl[1] + agg[1] : excl[2] + agg[2]);
@@ -80,8 +84,8 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
 
         int32_t mst = P.st;
         if (mst == HONU_OK) {  // as honu_decode_tables: offsets first, then the capacity check
-            if (P.nacl) P.R.u64(OFF(acl_off), ao);
-            if (P.nreg) P.R.u64(OFF(regions_off), ro);
+            if (P.nacl) O.meta[i].acl_off = ao;
+            if (P.nreg) O.meta[i].regions_off = ro;
             if (ao + P.nacl > O.acl_cap || ro + P.nreg > O.reg_cap) mst = HONU_ERR_CAPACITY;
         }
         int32_t dst_ = P.data_status;
@@ -94,7 +98,6 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
                 doff_out = doff;
             }
         }
-        rows_out(ws, P.R, i0, n, O.meta);
         if (valid) {
             store_info(O.info + i, make_info(P, doff_out, dlen_out, dst_, mst));
             if (O.materialize) {

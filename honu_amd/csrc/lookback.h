@@ -61,21 +61,33 @@ HONU_DEV uint64_t lb_ticket(LbState *s) {
 // Tile t of the launch with per-column aggregates agg[c] (wave-uniform):
 // publishes them, returns the exclusive prefixes of the tile in excl[c] and
 // publishes the inclusive ones. status holds K words per tile.
+// lb_scan in two halves, so that a wave can do work that needs no offsets
+// between publishing its aggregates and waiting for its predecessors.
+template <int K>
+HONU_DEV void lb_publish(uint64_t *status, uint64_t t, uint32_t ep, const uint64_t (&agg)[K]) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int c = 0; c < K; c++)
+        if (lane == (uint32_t)c) lb_store(status + t * K + c, lb_word(t == 0 ? 2 : 1, ep, agg[c]));
+}
+template <int K>
+HONU_DEV void lb_resolve(uint64_t *status, uint64_t t, uint32_t ep, const uint64_t (&agg)[K],
+                         uint64_t (&excl)[K]);
+
 template <int K>
 HONU_DEV void lb_scan(uint64_t *status, uint64_t t, uint32_t ep, const uint64_t (&agg)[K],
                       uint64_t (&excl)[K]) {
+    lb_publish<K>(status, t, ep, agg);
+    lb_resolve<K>(status, t, ep, agg, excl);
+}
+
+template <int K>
+HONU_DEV void lb_resolve(uint64_t *status, uint64_t t, uint32_t ep, const uint64_t (&agg)[K],
+                         uint64_t (&excl)[K]) {
     const uint32_t lane = lane_id();
 #pragma unroll
     for (int c = 0; c < K; c++) excl[c] = 0;
-    if (t == 0) {
-#pragma unroll
-        for (int c = 0; c < K; c++)
-            if (lane == (uint32_t)c) lb_store(status + c, lb_word(2, ep, agg[c]));
-        return;
-    }
-#pragma unroll
-    for (int c = 0; c < K; c++)
-        if (lane == (uint32_t)c) lb_store(status + t * K + c, lb_word(1, ep, agg[c]));
+    if (t == 0) return;  // published as inclusive already
     int64_t top[K];
     bool done[K];
 #pragma unroll
