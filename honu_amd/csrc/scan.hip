@@ -10,9 +10,11 @@
 
 namespace honu {
 
-template <int K> struct ScanCfg;
-template <> struct ScanCfg<1> { static constexpr int ITEMS = 16; };
-template <> struct ScanCfg<3> { static constexpr int ITEMS = 4; };
+// rows per thread: 3-column scans of small batches use short tiles (more
+// workgroups in flight: the scan is latency bound there), large ones long
+// tiles (fewer tickets and look-back steps)
+constexpr int SCAN_ITEMS_1 = 16, SCAN_ITEMS_3_SHORT = 4, SCAN_ITEMS_3_LONG = 16;
+constexpr uint64_t SCAN_LONG_ROWS = 1ull << 19;
 
 // Inclusive scan across the 256 threads of a block; *total gets the sum.
 HONU_DEV uint64_t block_incl_scan(uint64_t v, uint64_t *sh, uint64_t *total) {
@@ -36,10 +38,9 @@ HONU_DEV uint64_t block_incl_scan(uint64_t v, uint64_t *sh, uint64_t *total) {
 // ticket (one per workgroup); a tile sums its rows, wave 0 turns the tile's
 // column sums into its exclusive prefixes with the decoupled look-back
 // (lookback.h) and the workgroup writes its rows. in may alias out.
-template <int K>
+template <int K, int ITEMS>
 __global__ __launch_bounds__(HONU_BLOCK) void k_scan_lb(const uint64_t *in, uint64_t n, uint64_t *out,
                                                         uint64_t *__restrict__ totals, ScanState S) {
-    constexpr int ITEMS = ScanCfg<K>::ITEMS;
     __shared__ uint64_t sh[HONU_WAVES_PER_BLOCK];
     __shared__ uint64_t pre[K];
     __shared__ uint32_t tile_sh;
@@ -94,26 +95,29 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_scan_lb(const uint64_t *in, uint
     if (threadIdx.x < HONU_WAVE) lb_finish(S.lb, S.status, S.words, t, ntiles, gridDim.x);
 }
 
-uint64_t scan_status_words(uint64_t n) {  // the most K * tiles of any column count
-    const uint64_t t3 = (n + HONU_BLOCK * ScanCfg<3>::ITEMS - 1) / (HONU_BLOCK * ScanCfg<3>::ITEMS);
-    const uint64_t t1 = (n + HONU_BLOCK * ScanCfg<1>::ITEMS - 1) / (HONU_BLOCK * ScanCfg<1>::ITEMS);
+uint64_t scan_status_words(uint64_t n) {  // the most K * tiles of any form
+    const uint64_t t3 = (n + HONU_BLOCK * SCAN_ITEMS_3_SHORT - 1) / (HONU_BLOCK * SCAN_ITEMS_3_SHORT);
+    const uint64_t t1 = (n + HONU_BLOCK * SCAN_ITEMS_1 - 1) / (HONU_BLOCK * SCAN_ITEMS_1);
     return 3 * t3 > t1 ? 3 * t3 + 3 : t1 + 3;
 }
 
-template <int K>
+template <int K, int ITEMS>
 static hipError_t scan_k(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *totals,
                          const ScanState &S, hipStream_t s) {
-    const uint64_t tiles = (n + HONU_BLOCK * ScanCfg<K>::ITEMS - 1) / (HONU_BLOCK * ScanCfg<K>::ITEMS);
+    const uint64_t tiles = (n + HONU_BLOCK * ITEMS - 1) / (HONU_BLOCK * ITEMS);
     const uint64_t b = tiles < (uint64_t)S.max_blocks ? tiles : (uint64_t)S.max_blocks;
-    hipLaunchKernelGGL(k_scan_lb<K>, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, in, n, out, totals, S);
+    hipLaunchKernelGGL((k_scan_lb<K, ITEMS>), dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, in, n,
+                       out, totals, S);
     return hipGetLastError();
 }
 
 hipError_t launch_scan(const uint64_t *in, uint64_t n, int K, uint64_t *out, uint64_t *totals,
                        const ScanState &S, hipStream_t s) {
     if (n == 0) return hipMemsetAsync(totals, 0, sizeof(uint64_t) * K, s);
-    if (K == 1) return scan_k<1>(in, n, out, totals, S, s);
-    if (K == 3) return scan_k<3>(in, n, out, totals, S, s);
+    if (K == 1) return scan_k<1, SCAN_ITEMS_1>(in, n, out, totals, S, s);
+    if (K == 3)
+        return n >= SCAN_LONG_ROWS ? scan_k<3, SCAN_ITEMS_3_LONG>(in, n, out, totals, S, s)
+                                   : scan_k<3, SCAN_ITEMS_3_SHORT>(in, n, out, totals, S, s);
     return hipErrorInvalidValue;
 }
 
