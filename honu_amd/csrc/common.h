@@ -199,67 +199,60 @@ HONU_DEV void wave_copy_bytes(uint8_t *__restrict__ dst, const uint8_t *__restri
 // page, so the over-read is always mapped.
 // NT: non-temporal cache policy, 0 none, 1 loads and stores, 2 loads only,
 // 3 stores only; 4: a misaligned source is read with one unaligned 16-byte
-// load per chunk instead of two aligned loads and a funnel
+// load per chunk instead of two aligned loads and a funnel.
+// The head bytes, the tail bytes and the first UNROLL x 64 chunks are all
+// loaded before any of them is stored, so a short segment (the common case
+// for Small records: 2.5 KB) costs one round trip, not three.
 template <int UNROLL = 4, int NT = 0>
 HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint64_t n) {
     if (n == 0) return;
+    constexpr bool NTL = NT == 1 || NT == 2, NTS = NT == 1 || NT == 3;
     const uint32_t lane = lane_id();
-    const uint64_t d0 = (uint64_t)dst;
-    uint64_t head = (16u - (d0 & 15u)) & 15u;
+    uint64_t head = (16u - ((uint64_t)dst & 15u)) & 15u;
     if (head > n) head = n;
-    if (head && lane < head) dst[lane] = src[lane];
-    dst += head;
-    src += head;
-    n -= head;
-    const uint64_t chunks = n >> 4;
-    const uint64_t tail = n & 15u;
-    u32x4 *__restrict__ d4 = reinterpret_cast<u32x4 *>(dst);
-    const uint32_t p = (uint32_t)((uint64_t)src & 15u);
-    // Every iteration issues all its loads before any store, with per-chunk
-    // predication instead of a serial remainder loop, so a short segment costs
-    // one round trip, not one per 1 KiB.
-    if (p == 0) {
-        const u32x4 *__restrict__ s4 = reinterpret_cast<const u32x4 *>(src);
-        for (uint64_t c = lane; c < chunks; c += UNROLL * HONU_WAVE) {
-            u32x4 v[UNROLL];
-#pragma unroll
-            for (int u = 0; u < UNROLL; u++)
-                if (c + u * HONU_WAVE < chunks) v[u] = ld16<(NT == 1 || NT == 2)>(&s4[c + u * HONU_WAVE]);
-#pragma unroll
-            for (int u = 0; u < UNROLL; u++)
-                if (c + u * HONU_WAVE < chunks) st16<(NT == 1 || NT == 3)>(&d4[c + u * HONU_WAVE], v[u]);
+    const uint64_t chunks = (n - head) >> 4;
+    const uint64_t tail = (n - head) & 15u;
+    const uint64_t t0 = head + (chunks << 4);
+    u32x4 *__restrict__ d4 = reinterpret_cast<u32x4 *>(dst + head);
+    const uint8_t *bsrc = src + head;
+    const uint32_t p = (uint32_t)((uint64_t)bsrc & 15u);  // wave-uniform
+    const u32x4 *__restrict__ s4 = reinterpret_cast<const u32x4 *>(bsrc - p);
+    auto load = [&](uint64_t c, u32x4 &a, u32x4 &b) {
+        if (NT == 4 && p) {
+            a = *reinterpret_cast<const u32x4u *>(bsrc + 16 * c);
+        } else {
+            a = ld16<NTL>(&s4[c]);
+            if (p) b = ld16<NTL>(&s4[c + 1]);
         }
-    } else if (NT == 4) {
-        for (uint64_t c = lane; c < chunks; c += UNROLL * HONU_WAVE) {
-            u32x4 v[UNROLL];
+    };
+    auto store = [&](uint64_t c, const u32x4 &a, const u32x4 &b) {
+        st16<NTS>(&d4[c], (p == 0 || NT == 4) ? a : funnel16(a, b, p));
+    };
+    // round 0: edges and the first chunks
+    uint8_t hv = 0, tv = 0;
+    if (lane < head) hv = src[lane];
+    if (lane < tail) tv = src[t0 + lane];
+    {
+        u32x4 a[UNROLL], b[UNROLL];
 #pragma unroll
-            for (int u = 0; u < UNROLL; u++)
-                if (c + u * HONU_WAVE < chunks)
-                    v[u] = *reinterpret_cast<const u32x4u *>(src + 16 * (c + u * HONU_WAVE));
+        for (int u = 0; u < UNROLL; u++)
+            if (lane + u * HONU_WAVE < chunks) load(lane + u * HONU_WAVE, a[u], b[u]);
+        if (lane < head) dst[lane] = hv;
 #pragma unroll
-            for (int u = 0; u < UNROLL; u++)
-                if (c + u * HONU_WAVE < chunks) d4[c + u * HONU_WAVE] = v[u];
-        }
-    } else {
-        const u32x4 *__restrict__ s4 = reinterpret_cast<const u32x4 *>(src - p);
-        for (uint64_t c = lane; c < chunks; c += UNROLL * HONU_WAVE) {
-            u32x4 lo[UNROLL], hi[UNROLL];
-#pragma unroll
-            for (int u = 0; u < UNROLL; u++) {
-                if (c + u * HONU_WAVE < chunks) {
-                    lo[u] = ld16<(NT == 1 || NT == 2)>(&s4[c + u * HONU_WAVE]);
-                    hi[u] = ld16<(NT == 1 || NT == 2)>(&s4[c + u * HONU_WAVE + 1]);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < UNROLL; u++)
-                if (c + u * HONU_WAVE < chunks)
-                    st16<(NT == 1 || NT == 3)>(&d4[c + u * HONU_WAVE], funnel16(lo[u], hi[u], p));
-        }
+        for (int u = 0; u < UNROLL; u++)
+            if (lane + u * HONU_WAVE < chunks) store(lane + u * HONU_WAVE, a[u], b[u]);
+        if (lane < tail) dst[t0 + lane] = tv;
     }
-    if (tail) {
-        const uint64_t t0 = chunks << 4;
-        if (lane < tail) dst[t0 + lane] = src[t0 + lane];
+    // the rest: every iteration issues all its loads before any store, with
+    // per-chunk predication instead of a serial remainder loop
+    for (uint64_t c = lane + UNROLL * HONU_WAVE; c < chunks; c += UNROLL * HONU_WAVE) {
+        u32x4 a[UNROLL], b[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++)
+            if (c + u * HONU_WAVE < chunks) load(c + u * HONU_WAVE, a[u], b[u]);
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++)
+            if (c + u * HONU_WAVE < chunks) store(c + u * HONU_WAVE, a[u], b[u]);
     }
 }
 
