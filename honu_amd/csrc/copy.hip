@@ -38,12 +38,14 @@ struct EncodeSegments {
         // the header/tail encoder may still be running on another stream:
         // its HONU_ERR_CAPACITY is not visible here, so the capacity check
         // is repeated (nothing is written past out_cap)
-        if (status[i] != HONU_OK || out_off[i + 1] > out_cap) return false;
+        // every field loaded unconditionally (all in one round trip)
+        const int32_t st = status[i];
+        const uint64_t o0 = out_off[i], o1 = out_off[i + 1];
         const uint64_t s = payload_off[i];
         len = payload_off[i + 1] - s;
         src = payload + s;
-        dst = out + out_off[i] + 1 + uvarint_len(len);
-        return len != 0;
+        dst = out + o0 + 1 + uvarint_len(len);
+        return st == HONU_OK && o1 <= out_cap && len != 0;
     }
 };
 
@@ -61,11 +63,11 @@ struct DecodeSegments {
     HONU_DEV uint64_t end(uint64_t i, uint64_t total_abs) const { return i + 1 < n_ ? offs[3 * i + 5] : total_abs; }
     uint64_t n_;
     HONU_DEV bool get(uint64_t i, uint64_t &len, const uint8_t *&src, uint8_t *&dst) const {
-        if (info[i].data_status != HONU_OK) return false;
+        const int32_t st = info[i].data_status;  // every field in one round trip
         len = info[i].data_len;
         src = rec + scratch[i].data_src;
         dst = data + offs[3 * i + 2];
-        return len != 0;
+        return st == HONU_OK && len != 0;
     }
 };
 
@@ -82,11 +84,11 @@ struct SpanSegments {
     HONU_DEV uint64_t lo() const { return 0; }
     HONU_DEV uint64_t end(uint64_t i, uint64_t total_abs) const { (void)total_abs; return offs[i + 1]; }
     HONU_DEV bool get(uint64_t i, uint64_t &len, const uint8_t *&src, uint8_t *&dst) const {
-        if (info[i].data_status != HONU_OK) return false;
+        const int32_t st = info[i].data_status;  // every field in one round trip
         len = info[i].data_len;
         src = rec + scratch[i].data_src;
         dst = data + offs[i];
-        return len != 0;
+        return st == HONU_OK && len != 0;
     }
 };
 
@@ -114,13 +116,25 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t 
         if (seg.start(mid) <= lo) a = mid;
         else b = mid;
     }
+    // A segment's descriptors (start, then status / lengths / pointers) are
+    // loaded one segment ahead: issued before the current segment's copy, they
+    // arrive with its loads, so a short segment costs one round trip instead
+    // of three (start -> descriptors -> bytes).
+    uint64_t s_nx = seg.start(a), len_nx = 0;
+    const uint8_t *src_nx = nullptr;
+    uint8_t *dst_nx = nullptr;
+    bool ok_nx = seg.get(a, len_nx, src_nx, dst_nx);
     for (uint64_t i = a; i < n; i++) {
-        const uint64_t s = seg.start(i);
+        const uint64_t s = s_nx, len = len_nx;
+        const uint8_t *src = src_nx;
+        uint8_t *dst = dst_nx;
+        const bool ok = ok_nx;
         if (s >= hi) break;
-        uint64_t len;
-        const uint8_t *src;
-        uint8_t *dst;
-        if (!seg.get(i, len, src, dst)) continue;
+        if (i + 1 < n) {
+            s_nx = seg.start(i + 1);
+            ok_nx = seg.get(i + 1, len_nx, src_nx, dst_nx);
+        }
+        if (!ok) continue;
         const uint64_t x = s > lo ? s : lo;
         const uint64_t e = s + len;
         const uint64_t y = e < hi ? e : hi;
