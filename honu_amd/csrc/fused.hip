@@ -18,6 +18,9 @@
 namespace honu {
 
 #define OFF(f) ((int)offsetof(honu_meta, f))
+#ifndef FILL_U
+#define FILL_U 4  // ACL entries per lane in flight in the fill
+#endif
 
 // ------------------------------------------------------------------------
 // decode: Object.Metadata() + Data() + Tombstone() + StorageVersion()
@@ -152,12 +155,12 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         }
         uint64_t ftot;
         const uint64_t fpre = wave_excl(fast ? P.nacl : 0, ftot);
-        constexpr int U = 4;  // entries per lane in flight
+        constexpr int U = FILL_U;  // entries per lane in flight
         if (!(O.dbg & 1))
         for (uint64_t e0 = 0; e0 < ftot; e0 += U * HONU_WAVE) {  // wave-uniform
-            u32x4 a[U], b[U];
+            u32x4 id[U];
+            uint32_t pm[U];
             uint64_t dst[U];
-            uint32_t sh[U];
 #pragma unroll
             for (int k = 0; k < U; k++) {
                 const uint64_t e = e0 + lane + HONU_WAVE * k;
@@ -165,28 +168,22 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
                 const uint64_t rp = shfl64(fpre, r), ra = shfl64(apos, r), rao = shfl64(ao, r);
                 const uint64_t j = e - rp;
                 const uint64_t q = ra + 18 * j + 1;  // ClientID, then Permissions at q + 16
-                sh[k] = (uint32_t)(q & 15);
                 dst[k] = rao + j;
-                if (e < ftot) {
-                    a[k] = *reinterpret_cast<const u32x4 *>(rec + (q & ~15ull));
-                    b[k] = *reinterpret_cast<const u32x4 *>(rec + (q & ~15ull) + 16);
+                if (e < ftot) {  // one unaligned 16-byte load + one byte
+                    id[k] = *reinterpret_cast<const u32x4u *>(rec + q);
+                    pm[k] = rec[q + 16];
                 }
             }
 #pragma unroll
             for (int k = 0; k < U; k++) {
                 const uint64_t e = e0 + lane + HONU_WAVE * k;
                 if (e < ftot) {
-                    uint64_t lo, hi;
-                    window16(a[k], b[k], sh[k], lo, hi);
-                    const uint32_t s = sh[k];
-                    const uint32_t bw = s < 4 ? b[k].x : (s < 8 ? b[k].y : (s < 12 ? b[k].z : b[k].w));
-                    const uint32_t pm = (bw >> (8 * (s & 3))) & 0xFF;
                     uint32_t *d = reinterpret_cast<uint32_t *>(O.acl + dst[k]);
-                    d[0] = (uint32_t)lo;
-                    d[1] = (uint32_t)(lo >> 32);
-                    d[2] = (uint32_t)hi;
-                    d[3] = (uint32_t)(hi >> 32);
-                    d[4] = pm | (1u << 8);
+                    d[0] = id[k].x;
+                    d[1] = id[k].y;
+                    d[2] = id[k].z;
+                    d[3] = id[k].w;
+                    d[4] = pm[k] | (1u << 8);
                 }
             }
         }
