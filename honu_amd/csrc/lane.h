@@ -205,49 +205,55 @@ HONU_DEV uint32_t uvarint_bytes(uint64_t x, uint64_t &lo, uint64_t &hi) {
 
 // A lane-private byte stream into global memory at an arbitrary offset. Bytes
 // gather in a 16-byte register chunk aligned to the destination's 16-byte
-// grid; full chunks leave as one 16-byte store, the two partial chunks at the
-// ends as byte stores (their other bytes belong to neighbours).
+// grid; full chunks leave as one 16-byte store. The two partial chunks at the
+// ends (their other bytes belong to neighbours) leave as narrower stores, both
+// in finish(): the head chunk is parked in registers when it fills, so every
+// put() carries one 16-byte store and no partial-store code (the kernel's size
+// is its instruction-cache footprint).
 struct LaneWriter {
     uint8_t *out;
     uint64_t cpos;    // absolute offset of the current chunk (16-aligned)
     uint32_t f;       // next byte index in the chunk
     uint32_t first;   // first byte of the chunk this stream owns
     uint64_t a0, a1;  // chunk bytes 0..7, 8..15
+    uint64_t hpos;    // parked head chunk (hfirst != 0): offset, first byte, bytes
+    uint32_t hfirst;
+    uint64_t h0, h1;
 
     HONU_DEV void init(uint8_t *o, uint64_t pos) {
         out = o;
         cpos = pos & ~15ull;
         f = first = (uint32_t)(pos & 15);
         a0 = a1 = 0;
+        hfirst = 0;
     }
-    // bytes [from, to) of the chunk with the widest aligned stores that fit
-    // (at most 1 + 1 + 1 + 1 + 1 + 1 stores instead of one per byte)
-    HONU_DEV void store_bytes(uint32_t from, uint32_t to) {
-        uint8_t *p = out + cpos;
+    // bytes [from, to) of the chunk (b0, b1) at p with the widest aligned
+    // stores that fit (at most 6 stores instead of one per byte)
+    static HONU_DEV void store_bytes(uint8_t *p, uint32_t from, uint32_t to, uint64_t b0, uint64_t b1) {
         uint32_t j = from;
         auto bytes_at = [&](uint32_t k, uint32_t n) -> uint64_t {  // n <= 8, k + n <= 16
-            uint64_t v = k < 8 ? (a0 >> (8 * k)) | (k ? a1 << (64 - 8 * k) : 0) : a1 >> (8 * (k - 8));
+            uint64_t v = k < 8 ? (b0 >> (8 * k)) | (k ? b1 << (64 - 8 * k) : 0) : b1 >> (8 * (k - 8));
             return n == 8 ? v : v & ((1ull << (8 * n)) - 1);
         };
         if ((j & 1) && j < to) { p[j] = (uint8_t)bytes_at(j, 1); j += 1; }
         if ((j & 2) && j + 2 <= to) { *reinterpret_cast<uint16_t *>(p + j) = (uint16_t)bytes_at(j, 2); j += 2; }
         if ((j & 4) && j + 4 <= to) { *reinterpret_cast<uint32_t *>(p + j) = (uint32_t)bytes_at(j, 4); j += 4; }
-        if (j == 0 && to == 16) {
-            *reinterpret_cast<u32x4 *>(p) = u32x4{(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32)};
-            return;
-        }
         if (j + 8 <= to) { *reinterpret_cast<uint64_t *>(p + j) = bytes_at(j, 8); j += 8; }
         if (j + 4 <= to) { *reinterpret_cast<uint32_t *>(p + j) = (uint32_t)bytes_at(j, 4); j += 4; }
         if (j + 2 <= to) { *reinterpret_cast<uint16_t *>(p + j) = (uint16_t)bytes_at(j, 2); j += 2; }
         if (j < to) p[j] = (uint8_t)bytes_at(j, 1);
     }
     HONU_DEV void flush() {
-        if (first == 0)
+        if (first == 0) {
             *reinterpret_cast<u32x4 *>(out + cpos) =
                 u32x4{(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32)};
-        else
-            store_bytes(first, 16);
-        first = 0;
+        } else {  // the head chunk: parked until finish()
+            hpos = cpos;
+            hfirst = first;
+            h0 = a0;
+            h1 = a1;
+            first = 0;
+        }
         cpos += 16;
     }
     // append the low n (1..8) bytes of v (bytes above n must be zero)
@@ -280,25 +286,34 @@ struct LaneWriter {
         put(lo, n < 8 ? n : 8);
         if (n > 8) put(hi, n - 8);
     }
-    // raw bytes src[0, len) (global, any alignment). Words are loaded 64 bytes
-    // at a time before any of them is written out: the output stores may
-    // alias for the compiler, so loads cannot move past them on their own.
+    // raw bytes src[0, len) (global, any alignment). 64 bytes at a time are
+    // loaded as five aligned 16-byte blocks before any of them is written out
+    // (the output stores may alias for the compiler, so loads cannot move past
+    // them on their own); each memory instruction is a per-lane scattered
+    // access, so fewer, wider ones are what the address unit needs.
     HONU_DEV void run(const uint8_t *src, uint64_t len) {
-        const uint64_t a = (uint64_t)src & 7;
-        const uint64_t *w = reinterpret_cast<const uint64_t *>(src - a);
-        const uint64_t nw = (a + len + 7) >> 3;  // aligned words holding the run
+        const uint64_t a = (uint64_t)src & 15;
+        const u32x4 *w = reinterpret_cast<const u32x4 *>(src - a);
+        const uint64_t nw = (a + len + 15) >> 4;  // aligned blocks holding the run
+        const uint32_t sh = (uint32_t)(a & 7) * 8, hw = (uint32_t)(a >> 3);
         for (uint64_t k = 0; k < len; k += 64) {
-            const uint64_t q0 = (a + k) >> 3;
-            uint64_t x[9];
+            const uint64_t q0 = (a + k) >> 4;
+            uint64_t x[11];
 #pragma unroll
-            for (int j = 0; j < 9; j++) x[j] = (q0 + j < nw) ? w[q0 + j] : 0;
-            const uint32_t sh = (uint32_t)(a & 7) * 8;  // same phase every batch
+            for (int j = 0; j < 5; j++) {
+                u32x4 v{0, 0, 0, 0};
+                if (q0 + j < nw) v = w[q0 + j];
+                x[2 * j] = ((uint64_t)v.y << 32) | v.x;
+                x[2 * j + 1] = ((uint64_t)v.w << 32) | v.z;
+            }
+            x[10] = 0;
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 const uint64_t off = k + 8 * j;
                 if (off < len) {
                     const uint64_t take = len - off < 8 ? len - off : 8;
-                    uint64_t v = sh ? (x[j] >> sh) | (x[j + 1] << (64 - sh)) : x[j];
+                    const uint64_t lo = hw ? x[j + 1] : x[j], hi = hw ? x[j + 2] : x[j + 1];
+                    uint64_t v = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
                     if (take < 8) v &= (1ull << (8 * take)) - 1;
                     put(v, (uint32_t)take);
                 }
@@ -310,7 +325,9 @@ struct LaneWriter {
         run(var + sp.off, sp.len);
     }
     HONU_DEV void finish() {
-        if (f > first) store_bytes(first, f);
+        if (hfirst) store_bytes(out + hpos, hfirst, 16, h0, h1);
+        hfirst = 0;
+        if (f > first) store_bytes(out + cpos, first, f, a0, a1);
     }
     // absolute position of the next byte
     HONU_DEV uint64_t pos() const { return cpos + f; }
@@ -323,6 +340,22 @@ struct LaneWriter {
     }
 };
 
+
+// Timing build only (-DHONU_ENC_TIMING, tools/enc_timing.py): lane 0 of every
+// wave records s_memrealtime at fixed points of its encode.
+#ifdef HONU_ENC_TIMING
+#define ENC_STAMPS 8
+static __device__ uint64_t g_enc_stamps[1 << 16][ENC_STAMPS];  // per translation unit
+#define ESTAMP(k)                                                                             \
+    do {                                                                                      \
+        const uint64_t wid_ = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;    \
+        if (__lane_id() == 0 && wid_ < (1 << 16)) g_enc_stamps[wid_][k] = wall_clock64();     \
+    } while (0)
+#else
+#define ESTAMP(k) \
+    do {          \
+    } while (0)
+#endif
 
 // ------------------------------------------------------------------------
 // encode of one record by one lane (object.go:24-45, metadata.go:108-200),
@@ -406,6 +439,7 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
                                      uint64_t beg, uint64_t end, uint8_t *__restrict__ out) {
 #define OFF(f) ((int)offsetof(honu_meta, f))
     uint64_t acl_ret = 0;
+    ESTAMP(1);  // row loaded
     const uint8_t *mb = reinterpret_cast<const uint8_t *>(&m);
     const uint32_t pr = m.present;
     {  // header: version byte + uvarint(len data)   object.go:30,35
@@ -447,12 +481,14 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
         W.byte(0);
     }
     W.frame(var, m.mime);                                           // :130
+    ESTAMP(2);  // header .. MIME
     W.put16(ld64(mb + OFF(owner)), ld64(mb + OFF(owner) + 8));      // :135
     W.put16(ld64(mb + OFF(group)), ld64(mb + OFF(group) + 8));      // :140
     W.byte(m.permissions);                                          // :145
     const uint64_t na = m.acl_count, ao = m.acl_off;
     W.uv(na);                                                       // :151
     const uint64_t nr = m.regions_count, ro = m.regions_off;
+    ESTAMP(3);  // Owner .. ACL count
     if constexpr (SKIP_ACL) {
         const uint64_t P = W.pos();
         uint64_t sfx = uvarint_len(nr) + 3 + 1 + uvarint_len(zigzag(m.created)) +
@@ -477,26 +513,22 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
             acl_ret = P | ACL_ALL_PRESENT;
             const uint64_t hend = ((P + 15) & ~15ull) < E ? ((P + 15) & ~15ull) : E;
             const uint64_t T = (E & ~15ull) > hend ? (E & ~15ull) : hend;
-            for (uint64_t x = P; x < E;) {
-                if (x == hend && x < T) {
-                    W.jump(T);
-                    x = T;
-                    continue;
+            // the list's encoding at both ends (acl_chunk: 16 bytes from the
+            // <= 2 entries they straddle), both loaded at once
+            const u32x4 hv = acl_chunk(acl + ao, na, P, P);
+            const u32x4 tv = E > T ? acl_chunk(acl + ao, na, P, T) : u32x4{0, 0, 0, 0};
+            auto put_n = [&](const u32x4 &v, uint32_t cnt) {  // the first cnt (< 16) bytes of v
+                const uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
+                if (cnt >= 8) {
+                    W.put(lo, 8);
+                    if (cnt > 8) W.put(hi & ((1ull << (8 * (cnt - 8))) - 1), cnt - 8);
+                } else if (cnt) {
+                    W.put(lo & ((1ull << (8 * cnt)) - 1), cnt);
                 }
-                const uint64_t j = (x - P) / 18;
-                uint32_t d[5];
-                acl_enc_words(acl + ao + j, d);
-                const uint64_t lo = ((uint64_t)d[1] << 32) | d[0], hi = ((uint64_t)d[3] << 32) | d[2];
-                const uint64_t stop = P + 18 * (j + 1) < (x < hend ? hend : E) ? P + 18 * (j + 1)
-                                                                             : (x < hend ? hend : E);
-                for (; x < stop; x++) {
-                    const uint32_t k = (uint32_t)(x - P - 18 * j);
-                    const uint32_t bv = k < 8 ? (uint32_t)(lo >> (8 * k))
-                                              : k < 16 ? (uint32_t)(hi >> (8 * (k - 8)))
-                                                       : d[4] >> (8 * (k - 16));
-                    W.byte(bv);
-                }
-            }
+            };
+            put_n(hv, (uint32_t)(hend - P));
+            if (T > hend) W.jump(T);  // the whole chunks in between are k_encode_acl_grp's
+            put_n(tv, (uint32_t)(E - T));
         } else {
             acl_ret = P;
             W.jump(E);
@@ -526,6 +558,7 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
         }
     }
     }
+    ESTAMP(4);  // ACL list (ends)
     W.uv(nr);                                                       // :164, region.go:137-152
     for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
         uint32_t r8[8];
@@ -535,6 +568,7 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
         for (int j = 0; j < 8; j++)
             if (k0 + j < nr) W.uv(r8[j]);
     }
+    ESTAMP(5);  // regions
     if (pr & HONU_HAS_PUBLISHER) {                                  // :169, provenance.go:34-57
         W.byte(1);
         W.put16(ld64(mb + OFF(publisher_id)), ld64(mb + OFF(publisher_id) + 8));
@@ -544,6 +578,7 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
     } else {
         W.byte(0);
     }
+    ESTAMP(6);  // publisher
     if (pr & HONU_HAS_ENCRYPTION) {                                 // :174, encryption.go:51-89
         W.byte(1);
         W.frame(var, m.public_key_id);
@@ -567,6 +602,7 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
     W.uv(zigzag(m.created));                                        // :189
     W.uv(zigzag(m.modified));                                       // :194
     W.finish();
+    ESTAMP(7);  // encryption .. end
     return acl_ret;
 }
 #undef OFF

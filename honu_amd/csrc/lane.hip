@@ -18,6 +18,7 @@ HONU_DEV void k_encode_meta_lane_one(uint64_t i, const honu_meta *__restrict__ m
     const uint64_t *__restrict__ payload_off, uint64_t n, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status,
     uint64_t *__restrict__ acl_out) {
+    ESTAMP(0);  // entered
     if (status[i] != HONU_OK) return;
     const uint64_t beg = out_off[i], end = out_off[i + 1];
     if (end > out_cap) {
@@ -183,3 +184,11 @@ hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, co
 }
 
 }  // namespace honu
+
+#ifdef HONU_ENC_TIMING
+extern "C" int32_t honu_debug_enc_stamps(void *host, uint64_t waves) {
+    if (waves > (1 << 16)) waves = 1 << 16;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(honu::g_enc_stamps),
+                               waves * ENC_STAMPS * sizeof(uint64_t)) == hipSuccess ? 0 : -3;
+}
+#endif
