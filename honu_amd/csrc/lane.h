@@ -205,12 +205,19 @@ HONU_DEV uint32_t uvarint_bytes(uint64_t x, uint64_t &lo, uint64_t &hi) {
 
 // A lane-private byte stream into global memory at an arbitrary offset. Bytes
 // gather in a 16-byte register chunk aligned to the destination's 16-byte
-// grid; full chunks leave as one 16-byte store. The two partial chunks at the
-// ends (their other bytes belong to neighbours) leave as narrower stores, both
-// in finish(): the head chunk is parked in registers when it fills, so every
-// put() carries one 16-byte store and no partial-store code (the kernel's size
-// is its instruction-cache footprint).
-struct LaneWriter {
+// grid. The two partial chunks at the ends (their other bytes belong to
+// neighbours) leave as narrower stores, both in finish(): the head chunk is
+// parked in registers when it fills, so a put() carries no partial-store code
+// (the kernel's size is its instruction-cache footprint).
+// R == 0: every full chunk leaves as one 16-byte store where it fills.
+// R > 0: full chunks go to a per-lane LDS ring of R chunks (slot-major, lanes
+// adjacent) and leave in drain(), which the caller places at points every
+// lane passes with fewer than R new chunks: the stores then issue from a few
+// places with most lanes active, instead of from every put() with the few
+// lanes whose chunk just filled (each store instruction costs the address
+// unit about the same however many lanes it carries).
+template <int R>
+struct LaneWriterT {
     uint8_t *out;
     uint64_t cpos;    // absolute offset of the current chunk (16-aligned)
     uint32_t f;       // next byte index in the chunk
@@ -219,6 +226,8 @@ struct LaneWriter {
     uint64_t hpos;    // parked head chunk (hfirst != 0): offset, first byte, bytes
     uint32_t hfirst;
     uint64_t h0, h1;
+    u32x4 *ring;      // R > 0: this lane's slot 0 (slot k at ring[k * HONU_BLOCK])
+    uint32_t nch;     // R > 0: full chunks in the ring, ending just before cpos
 
     HONU_DEV void init(uint8_t *o, uint64_t pos) {
         out = o;
@@ -226,7 +235,9 @@ struct LaneWriter {
         f = first = (uint32_t)(pos & 15);
         a0 = a1 = 0;
         hfirst = 0;
+        nch = 0;
     }
+    HONU_DEV void set_ring(u32x4 *r) { ring = r; }
     // bytes [from, to) of the chunk (b0, b1) at p with the widest aligned
     // stores that fit (at most 6 stores instead of one per byte)
     static HONU_DEV void store_bytes(uint8_t *p, uint32_t from, uint32_t to, uint64_t b0, uint64_t b1) {
@@ -245,8 +256,13 @@ struct LaneWriter {
     }
     HONU_DEV void flush() {
         if (first == 0) {
-            *reinterpret_cast<u32x4 *>(out + cpos) =
-                u32x4{(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32)};
+            const u32x4 v{(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32)};
+            if constexpr (R > 0) {
+                ring[((cpos >> 4) & (R - 1)) * HONU_BLOCK] = v;
+                nch++;
+            } else {
+                *reinterpret_cast<u32x4 *>(out + cpos) = v;
+            }
         } else {  // the head chunk: parked until finish()
             hpos = cpos;
             hfirst = first;
@@ -297,6 +313,7 @@ struct LaneWriter {
         const uint64_t nw = (a + len + 15) >> 4;  // aligned blocks holding the run
         const uint32_t sh = (uint32_t)(a & 7) * 8, hw = (uint32_t)(a >> 3);
         for (uint64_t k = 0; k < len; k += 64) {
+            drain();  // <= R - 1 chunks since the last one (see encode_record_lane)
             const uint64_t q0 = (a + k) >> 4;
             uint64_t x[11];
 #pragma unroll
@@ -324,7 +341,17 @@ struct LaneWriter {
         uv(sp.len);
         run(var + sp.off, sp.len);
     }
+    // the ring's chunks to memory (no-op for R == 0)
+    HONU_DEV void drain() {
+        if constexpr (R > 0) {
+            const uint64_t p0 = cpos - 16ull * nch;
+            for (uint32_t k = 0; k < nch; k++)
+                *reinterpret_cast<u32x4 *>(out + p0 + 16 * k) = ring[(((p0 >> 4) + k) & (R - 1)) * HONU_BLOCK];
+            nch = 0;
+        }
+    }
     HONU_DEV void finish() {
+        drain();
         if (hfirst) store_bytes(out + hpos, hfirst, 16, h0, h1);
         hfirst = 0;
         if (f > first) store_bytes(out + cpos, first, f, a0, a1);
@@ -339,6 +366,7 @@ struct LaneWriter {
         a0 = a1 = 0;
     }
 };
+using LaneWriter = LaneWriterT<0>;
 
 
 // Timing build only (-DHONU_ENC_TIMING, tools/enc_timing.py): lane 0 of every
@@ -432,11 +460,18 @@ HONU_DEV uint64_t encode_tail_bytes_noacl(const honu_meta &m, const uint32_t *__
 // (| ACL_ALL_PRESENT when every entry is present: the partial 16-byte chunks
 // at both ends of the list are then written here) and resume at
 // end - (bytes after the list), computed from the row and regions.
-template <bool SKIP_ACL>
+// R: the writer's LDS ring (LaneWriterT; ring = this lane's slot 0). Drains
+// sit where every lane has written fewer than 112 bytes since the previous one
+// (< 8 chunks): between two drains at most one raw-run batch (64 bytes, run()
+// drains before each) plus fixed fields of <= 48 bytes, or <= 96 bytes of
+// fixed fields (uvarints counted at their 10-byte maximum).
+template <bool SKIP_ACL, int R>
 HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restrict__ var,
                                      const honu_acl *__restrict__ acl,
                                      const uint32_t *__restrict__ reg, uint64_t dlen,
-                                     uint64_t beg, uint64_t end, uint8_t *__restrict__ out) {
+                                     uint64_t beg, uint64_t end, uint8_t *__restrict__ out,
+                                     u32x4 *ring) {
+    static_assert(R == 0 || (R == 8 && SKIP_ACL), "drain spacing assumes 8 slots and no ACL entries");
 #define OFF(f) ((int)offsetof(honu_meta, f))
     uint64_t acl_ret = 0;
     ESTAMP(1);  // row loaded
@@ -449,8 +484,9 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
         for (uint32_t j = 0; j < hn; j++)
             out[beg + 1 + j] = (uint8_t)(j < 8 ? lo >> (8 * j) : hi >> (8 * (j - 8)));
     }
-    LaneWriter W;
+    LaneWriterT<R> W;
     W.init(out, beg + 1 + uvarint_len(dlen) + dlen);
+    W.set_ring(ring);
     W.byte(1);                                                      // EncodeStruct(meta)
     W.put16(ld64(mb + OFF(object_id)), ld64(mb + OFF(object_id) + 8));          // :110
     W.put16(ld64(mb + OFF(collection_id)), ld64(mb + OFF(collection_id) + 8));  // :115
@@ -471,6 +507,7 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
     } else {
         W.byte(0);
     }
+    W.drain();  // <= 33 + 63 bytes
     if (pr & HONU_HAS_SCHEMA) {                                     // :125, schema.go:30-53
         W.byte(1);
         W.frame(var, m.schema_name);
@@ -480,7 +517,9 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
     } else {
         W.byte(0);
     }
+    W.drain();  // <= 64 + 30
     W.frame(var, m.mime);                                           // :130
+    W.drain();  // <= 64
     ESTAMP(2);  // header .. MIME
     W.put16(ld64(mb + OFF(owner)), ld64(mb + OFF(owner) + 8));      // :135
     W.put16(ld64(mb + OFF(group)), ld64(mb + OFF(group) + 8));      // :140
@@ -526,7 +565,7 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
                     W.put(lo & ((1ull << (8 * cnt)) - 1), cnt);
                 }
             };
-            put_n(hv, (uint32_t)(hend - P));
+            put_n(hv, (uint32_t)(hend - P));  // <= 43 + 15 since the drain
             if (T > hend) W.jump(T);  // the whole chunks in between are k_encode_acl_grp's
             put_n(tv, (uint32_t)(E - T));
         } else {
@@ -564,20 +603,23 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
         uint32_t r8[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? reg[ro + k0 + j] : 0;
+        W.drain();  // <= 15 + 10 before the first batch, <= 40 after one
 #pragma unroll
         for (int j = 0; j < 8; j++)
             if (k0 + j < nr) W.uv(r8[j]);
     }
+    W.drain();
     ESTAMP(5);  // regions
     if (pr & HONU_HAS_PUBLISHER) {                                  // :169, provenance.go:34-57
         W.byte(1);
         W.put16(ld64(mb + OFF(publisher_id)), ld64(mb + OFF(publisher_id) + 8));
         W.put16(ld64(mb + OFF(client_id)), ld64(mb + OFF(client_id) + 8));
         W.frame(var, m.ip_address);
-        W.frame(var, m.user_agent);
+        W.frame(var, m.user_agent);  // run() drains: <= 33 + 10, then <= 64 + 10
     } else {
         W.byte(0);
     }
+    W.drain();  // <= 64
     ESTAMP(6);  // publisher
     if (pr & HONU_HAS_ENCRYPTION) {                                 // :174, encryption.go:51-89
         W.byte(1);
@@ -591,6 +633,7 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
     } else {
         W.byte(0);
     }
+    W.drain();  // <= 64 + 3; then <= 12 + 1 + 20 to finish()
     if (pr & HONU_HAS_COMPRESSION) {                                // :179, compression.go:40-53
         W.byte(1);
         W.byte(m.compression_alg);

@@ -12,12 +12,16 @@ namespace honu {
 // ------------------------------------------------------------------------
 // encode: header + Metadata tail (object.go:24-45, metadata.go:108-200)
 // ------------------------------------------------------------------------
+#ifndef ENC_RING
+#define ENC_RING 8  // chunks in the writer's LDS ring per lane (0: direct stores)
+#endif
+
 template <bool SKIP_ACL>
 HONU_DEV void k_encode_meta_lane_one(uint64_t i, const honu_meta *__restrict__ meta, const uint8_t *__restrict__ var,
     const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
     const uint64_t *__restrict__ payload_off, uint64_t n, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status,
-    uint64_t *__restrict__ acl_out) {
+    uint64_t *__restrict__ acl_out, u32x4 *ring) {
     ESTAMP(0);  // entered
     if (status[i] != HONU_OK) return;
     const uint64_t beg = out_off[i], end = out_off[i + 1];
@@ -34,7 +38,8 @@ HONU_DEV void k_encode_meta_lane_one(uint64_t i, const honu_meta *__restrict__ m
         for (int k = 0; k < 22; k++) dstr[k] = src[k];
     }
     const uint64_t dlen = payload_off[i + 1] - payload_off[i];
-    const uint64_t pos = encode_record_lane<SKIP_ACL>(m, var, acl, reg, dlen, beg, end, out);
+    const uint64_t pos = encode_record_lane<SKIP_ACL, SKIP_ACL ? ENC_RING : 0>(m, var, acl, reg, dlen, beg, end,
+                                                                           out, ring);
     if constexpr (SKIP_ACL) acl_out[i] = pos;
 }
 
@@ -45,9 +50,11 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
     const uint64_t *__restrict__ payload_off, uint64_t n, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status,
     uint64_t *__restrict__ acl_out) {
+    __shared__ u32x4 ring[(ENC_RING > 0 ? ENC_RING : 1) * HONU_BLOCK];  // slot-major, lanes adjacent
     for (uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * HONU_BLOCK)
-        k_encode_meta_lane_one<SKIP_ACL>(i, meta, var, acl, reg, payload_off, n, out, out_cap, out_off, status, acl_out);
+        k_encode_meta_lane_one<SKIP_ACL>(i, meta, var, acl, reg, payload_off, n, out, out_cap, out_off, status,
+                                         acl_out, ring + threadIdx.x);
 }
 
 #undef OFF
