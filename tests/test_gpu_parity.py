@@ -591,3 +591,38 @@ def test_concurrent_contexts_on_streams(oracle_lib):
         assert hobj._to_host(b["meta"], 352 * n, np.uint8).tobytes() == ometa.tobytes()
         assert hobj._to_host(b["info"], 32 * n, np.uint8).tobytes() == oinfo.tobytes()
         c.close()
+
+
+def test_encode_writer_drain_bounds(codec, oracle_lib):
+    """The lane encoder's LDS ring (lane.h LaneWriterT) holds 8 chunks between
+    drains; its drain placement assumes at most ~112 bytes per lane in between.
+    Records at that bound: every varint at its widest (10-byte VIDs and times,
+    5-byte PIDs, schema numbers and region ids), frames 63/64/65/128 bytes long
+    around the 64-byte run batches, up to 40 regions, empty frames right after
+    full batches, and payload lengths 0..15 so the tail starts at every phase
+    of the 16-byte grid. Encoded bytes bit-exact vs the oracle."""
+    from honu_amd.metadata import (AccessControl, Compression, Encryption, Metadata, Publisher,
+                                   Scalar, SchemaVersion, Version)
+    rng = np.random.default_rng(41)
+    M32, M64, MIN64 = 2**32 - 1, 2**64 - 1, -2**63
+    LENS = [0, 1, 63, 64, 65, 128]
+    metas, datas = [], []
+    for i in range(6 * 16 * 3):
+        ln = LENS[i % 6]
+        metas.append(Metadata(
+            ObjectID=rng.bytes(16), CollectionID=rng.bytes(16),
+            Version=Version(Scalar(M32, M64), M32, Scalar(M32, M64), True, MIN64),
+            Schema=SchemaVersion("s" * LENS[(i + 1) % 6], M32, M32, M32),
+            MIME="m" * LENS[(i + 2) % 6], Owner=rng.bytes(16), Group=rng.bytes(16), Permissions=255,
+            ACL=[AccessControl(rng.bytes(16), 7) for _ in range(i % 3)] or None,
+            WriteRegions=[M32] * ((i * 7) % 41) or None,
+            Publisher=Publisher(rng.bytes(16), rng.bytes(16), rng.bytes(ln) or None, "u" * LENS[(i + 3) % 6]),
+            Encryption=Encryption("k" * LENS[(i + 4) % 6], rng.bytes(LENS[(i + 5) % 6]) or None,
+                                  None, rng.bytes(ln) or None, 5, 1, 4),
+            Compression=Compression(1, MIN64), Flags=255, Created=MIN64, Modified=2**63 - 1))
+        datas.append(rng.bytes((i // 6) % 16) or None)
+    hb = pack_batch(metas, datas)
+    out, off, st = gpu_marshal(codec, hb)
+    oout, ooff, ost = oracle_lib.marshal_batch(hb)
+    assert np.array_equal(st, ost) and (st == 0).all()
+    assert np.array_equal(off, ooff) and out.tobytes() == oout.tobytes()
