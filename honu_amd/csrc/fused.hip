@@ -47,16 +47,20 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
     DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t lb_words) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * WIN_WAVE_BYTES];
+    __shared__ uint32_t last_flag;
     uint8_t *ws = smem + (threadIdx.x / HONU_WAVE) * WIN_WAVE_BYTES;
     const uint32_t lane = lane_id();
     const uint32_t ep = lb_epoch(lb);
     const uint64_t ntiles = (n + HONU_WAVE - 1) / HONU_WAVE;
+    const uint64_t waves = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
+    // every tile has a resident wave of its own: static tiles (lookback.h)
+    const bool stat = ntiles <= waves && !(O.dbg & 4);
     uint64_t t;
     uint64_t k_static = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + threadIdx.x / HONU_WAVE;
     for (;;) {
-        if (O.dbg & 4) {  // measurement only (with 2): static tiles, no tickets
+        if (stat || (O.dbg & 4)) {  // dbg 4: measurement only (with 2), static tiles at any size
             t = k_static;
-            k_static += gridDim.x * HONU_WAVES_PER_BLOCK;
+            k_static += waves;
         } else {
             t = lb_ticket(lb);
         }
@@ -188,7 +192,10 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
             }
         }
     }
-    if (!(O.dbg & 4)) lb_finish(lb, lb_status, lb_words, t, ntiles, gridDim.x * HONU_WAVES_PER_BLOCK);
+    if (stat)
+        lb_finish_blocks(lb, lb_status, lb_words, gridDim.x, &last_flag);
+    else if (!(O.dbg & 4))
+        lb_finish(lb, lb_status, lb_words, t, ntiles, (uint32_t)waves);
 }
 
 hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,

@@ -26,7 +26,7 @@ namespace honu {
 
 struct LbState {
     uint32_t ticket;  // next tile
-    uint32_t _unused;
+    uint32_t done;    // workgroups finished (static tiles, lb_finish_blocks)
     uint32_t epoch;
     uint32_t _pad;
 };
@@ -143,6 +143,32 @@ HONU_DEV void lb_finish(LbState *s, uint64_t *status, uint64_t status_words, uin
         for (uint64_t k = lane; k < status_words; k += HONU_WAVE) lb_store(status + k, 0);
     if (lane == 0) {
         __hip_atomic_store(&s->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&s->epoch, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Static tiles instead of tickets, for a launch whose tiles all fit its
+// resident waves (one tile per wave, tile = the wave's global index: every
+// predecessor a wave waits on belongs to a wave that is or will be resident,
+// as the whole grid fits the chip). Saves the launch-time burst of ticket
+// atomics on one address (~20 us for 2048 waves). The last workgroup to
+// finish (one atomic per workgroup) resets the count and advances the epoch;
+// on a wrap of the epoch it clears the status array first. Called by every
+// thread of the workgroup; flag: one word of LDS.
+HONU_DEV void lb_finish_blocks(LbState *s, uint64_t *status, uint64_t status_words, uint32_t nblocks,
+                               uint32_t *flag) {
+    __syncthreads();
+    if (threadIdx.x == 0)
+        *flag = __hip_atomic_fetch_add(&s->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                nblocks - 1;
+    __syncthreads();
+    if (!*flag) return;
+    const uint32_t e = (lb_epoch(s) + 1) & LB_EPOCH_MASK;
+    if (e == 0)
+        for (uint64_t k = threadIdx.x; k < status_words; k += blockDim.x) lb_store(status + k, 0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&s->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&s->epoch, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
 }

@@ -5,7 +5,12 @@ batch (many tiles) publishes words for every tile; 2^18 - 1 one-tile launches
 then advance the epoch to its wrap, where the status array must be cleared: a
 second wide batch with different counts decodes bit-exact only if no stale
 word of the first one is taken for its own. Also: batches of 1..300 tiles in
-a row, each checked against the oracle (every look-back window size)."""
+a row, each checked against the oracle (every look-back window size).
+
+Launches whose tiles all fit the resident waves take static tiles (one per
+wave, no ticket atomics, lookback.h lb_finish_blocks); larger ones take
+tickets (lb_finish). Both advance the same epoch: the last test alternates
+them, across an epoch wrap reached by static launches."""
 import numpy as np
 import pytest
 
@@ -86,3 +91,29 @@ def test_epoch_wrap_clears_stale_words(codec, oracle_lib):
     assert d2() == 0
     d2.check(oracle_lib, *wide2[:2])
     dt.check(oracle_lib, *tiny[:2])
+
+
+def test_static_and_ticket_launches_alternate(oracle_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    big_tiles = 2 * 4 * torch.cuda.get_device_properties(0).multi_processor_count + 40
+    c = hobj.Codec(0, 64 * big_tiles)
+    try:
+        wide1 = oracle_lib.marshal_batch(gen_host_batch(21, "small", 0, 64 * big_tiles - 5))
+        wide2 = oracle_lib.marshal_batch(gen_host_batch(22, "small", 0, 64 * big_tiles - 9))
+        mid = oracle_lib.marshal_batch(gen_host_batch(23, "small", 0, 64 * 150 - 3))
+        tiny = oracle_lib.marshal_batch(gen_host_batch(24, "small", 0, 64))
+        d1, d2 = _Dec(c, *wide1[:2]), _Dec(c, *wide2[:2])
+        dm, dt = _Dec(c, *mid[:2]), _Dec(c, *tiny[:2])
+        for d, b in ((d1, wide1), (dm, mid), (d2, wide2), (dt, tiny), (d1, wide1), (dm, mid)):
+            assert d() == 0
+            d.check(oracle_lib, *b[:2])
+        # static launches up to (and past) a wrap, then tickets over other data
+        for _ in range(EPOCHS - 1):
+            assert dt() == 0
+        assert d2() == 0
+        d2.check(oracle_lib, *wide2[:2])
+        assert dm() == 0
+        dm.check(oracle_lib, *mid[:2])
+    finally:
+        c.close()
