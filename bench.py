@@ -300,7 +300,7 @@ class Bench:
         self.last = (a, b, sl)
         return sl
 
-    FUSED_DECODE_MIN = 128 << 10  # as honu_decode_batch: fused from 128 K records
+    FUSED_DECODE_MIN = 48 << 10  # as honu_decode_batch: fused from 48 K records
 
     def fused_decode(self, n):
         d = self.args.decode

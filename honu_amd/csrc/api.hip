@@ -53,7 +53,7 @@ static bool aligned(const void *p, uintptr_t a) { return ((uintptr_t)p & (a - 1)
 // record_variant 5 runs the batch entries through the split kernels of
 // variant 0, 6 through the fused decode at every size; variant 0 picks by size
 static int split_rv(int rv) { return rv == 5 || rv == 6 ? 0 : rv; }
-#define FUSED_DECODE_MIN_RECORDS (128ull << 10)
+#define FUSED_DECODE_MIN_RECORDS (48ull << 10)
 // the A/B build (make ab: -DHONU_AB) adds the measurement-only kernel variants
 #ifdef HONU_AB
 #define HONU_AB_BUILD 1
@@ -461,9 +461,11 @@ int32_t honu_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
                           honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
                           uint64_t regions_cap, uint8_t *d_data, uint64_t data_cap,
                           uint64_t *d_totals, void *stream) {
-    // fused for batches of more than one round of resident waves (measured
-    // faster from ~128 K records; below, the split kernels' extra waves hide
-    // the walk's latency better), always with record_variant 6
+    // fused from 48 K records (measured: even with split at ~48 K, 3-5 % ahead
+    // at 62-65 K, and the 1M Large bench's 62 K-record chunks 4 % faster with
+    // one metadata launch per chunk beside the copies; below, the split
+    // kernels' extra waves hide the walk's latency better), always with
+    // record_variant 6
     const int rv = ctx ? ctx->geom.record_variant : 0;
     if (rv == 6 || (rv == 0 && n >= FUSED_DECODE_MIN_RECORDS)) {
         if (d_data && !aligned(d_data, 16)) return arg_fail("data arena must be 16-byte aligned");

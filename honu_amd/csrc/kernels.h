@@ -85,7 +85,7 @@ struct LaunchGeom {
     int copy_blocks;        // blocks of the byte-balanced copy kernel
     int copy_variant;       // copy engine variant (copy.hip: unroll depth / cache policy)
     int record_variant;     // per-record kernels: 0 auto (the fastest measured form
-                            // of each; honu_decode_batch single-launch from 128 K
+                            // of each; honu_decode_batch single-launch from 48 K
                             // records), 5 split decode, 6 single-launch decode
                             // at every size; A/B library only: 1 one record per
                             // wave, 2 per group of 16 lanes, 3 per lane, 4 group

@@ -194,7 +194,7 @@ uint64_t honu_ctx_max_records(const honu_ctx *ctx);
  * "copy_variant" (copy-engine variant, default 0), "record_variant" (how the
  * per-record metadata kernels map records to lanes: 0 auto — the fastest
  * measured form per kernel, with honu_decode_batch running the single-launch
- * decode for batches of 128 K records or more; 5 the split decode at every
+ * decode for batches of 48 K records or more; 5 the split decode at every
  * size; 6 the single-launch decode at every size; A/B builds add 1 one record
  * per wave, 2 one record per group of 16 lanes, 3 one record per lane, 4 lane
  * walks with group lists). Also
@@ -319,7 +319,7 @@ int32_t honu_decode_records(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t 
                             uint64_t regions_cap, int32_t materialize, uint64_t data_cap,
                             uint64_t *d_totals, void *stream);
 
-/* parse + fill in one call: from 128 K records honu_decode_records (+
+/* parse + fill in one call: from 48 K records honu_decode_records (+
  * honu_decode_payloads when d_data != NULL), below the split phases. */
 int32_t honu_decode_batch(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
                           uint64_t n, honu_meta *d_meta, honu_record_info *d_info,

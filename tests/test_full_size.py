@@ -4,7 +4,7 @@ configs[1] is 1M Small records encoded + decoded on one GPU; the other parity
 tests compare at most a few thousand records byte-exact and check the big
 batches through digests. Here the whole 1M Small batch (≈3.6 GB of records)
 goes through the default batch calls (size pass + scan + encode + payload
-copy; the single-launch decode, which honu_decode_batch picks from 128 K
+copy; the single-launch decode, which honu_decode_batch picks from 48 K
 records, both zero-copy and materialising) and every output is compared with
 oracle.marshal_batch / oracle.decode_batch: the records arena, offsets and
 statuses, all 352-byte rows, record info, the ACL and region tables, the
