@@ -300,7 +300,11 @@ class Bench:
         self.last = (a, b, sl)
         return sl
 
-    FUSED_DECODE_MIN = 48 << 10  # as honu_decode_batch: fused from 48 K records
+    # The pipeline's own crossover, above honu_decode_batch's 48 K: beside the
+    # other chunk's copies the split kernels are as fast on 62 K-record Large
+    # chunks (box-dependent, -2 % to +4 % for the single launch) and keep the
+    # encode copy faster (5.84 vs 5.63-5.67 TB/s, profiles/r02/crossover_static_tiles.txt)
+    FUSED_DECODE_MIN = 128 << 10
 
     def fused_decode(self, n):
         d = self.args.decode
