@@ -52,9 +52,9 @@ static bool aligned(const void *p, uintptr_t a) { return ((uintptr_t)p & (a - 1)
 
 // record_variant 5 runs the batch entries through the split kernels of
 // variant 0, 6 through the fused decode at every size; variant 0 picks by size
-static int split_rv(int rv) { return rv == 5 || rv == 6 ? 0 : rv; }
 #define FUSED_DECODE_MIN_RECORDS (48ull << 10)
-// the A/B build (make ab: -DHONU_AB) adds the measurement-only kernel variants
+// the A/B build (make ab: -DHONU_AB) adds the measurement-only copy variants and
+// the fused decode's measurement knobs
 #ifdef HONU_AB
 #define HONU_AB_BUILD 1
 #else
@@ -136,7 +136,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->geom.copy_blocks = env_int("HONU_COPY_BLOCKS", prop.multiProcessorCount * 2);
     c->geom.copy_variant = HONU_AB_BUILD ? env_int("HONU_COPY_VARIANT", 0) : 0;
     c->geom.record_variant = env_int("HONU_RECORD_VARIANT", 0);
-    if (!HONU_AB_BUILD && c->geom.record_variant != 5 && c->geom.record_variant != 6)
+    if (c->geom.record_variant != 5 && c->geom.record_variant != 6)
         c->geom.record_variant = 0;
     const uint64_t n = c->max_n;
     const uint64_t np = 0;
@@ -199,7 +199,7 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
     else if (!strcmp(name, "copy_variant") && value >= 0 && (value == 0 || HONU_AB_BUILD))
         ctx->geom.copy_variant = (int)value;
     else if (!strcmp(name, "record_variant") &&
-             (value == 0 || value == 5 || value == 6 || (HONU_AB_BUILD && value >= 1 && value <= 4)))
+             (value == 0 || value == 5 || value == 6))
         ctx->geom.record_variant = (int)value;
     else return arg_fail(name);
     return HONU_OK;
@@ -216,22 +216,6 @@ int32_t honu_encode_sizes(honu_ctx *ctx, const honu_meta *d_meta, uint64_t var_l
     if (n && (!d_meta || !d_payload_off || !d_sizes)) return arg_fail("null pointer");
     if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
     HIPCHK(hipSetDevice(ctx->device));
-    const int rv = split_rv(ctx->geom.record_variant);
-#ifdef HONU_AB
-    if (rv == 3) {
-        HIPCHK(launch_encode_sizes_lane(d_meta, var_len, d_acl, acl_len, d_regions, regions_len,
-                                        d_payload_off, n, d_sizes, d_status, ctx->geom.lane_blocks,
-                                        (hipStream_t)stream));
-        return HONU_OK;
-    }
-    if (rv == 1) {
-        HIPCHK(launch_encode_sizes(ctx->geom, d_meta, var_len, d_acl, acl_len, d_regions,
-                                   regions_len, d_payload_off, n, d_sizes, d_status,
-                                   (hipStream_t)stream));
-        return HONU_OK;
-    }
-#endif
-    (void)rv;
     HIPCHK(launch_encode_sizes_grp(d_meta, var_len, d_acl, acl_len, d_regions, regions_len,
                                    d_payload_off, n, d_sizes, d_status, ctx->geom.lane_blocks,
                                    (hipStream_t)stream));
@@ -257,27 +241,6 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
         return arg_fail("null pointer");
     if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
     HIPCHK(hipSetDevice(ctx->device));
-    const int rv = split_rv(ctx->geom.record_variant);
-#ifdef HONU_AB
-    if (rv == 2) {
-        HIPCHK(launch_encode_meta_grp(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
-                                      out_cap, d_out_off, d_status, ctx->geom.lane_blocks,
-                                      (hipStream_t)stream));
-        return HONU_OK;
-    }
-    if (rv == 3 || rv == 4) {
-        HIPCHK(launch_encode_meta_lane(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
-                                       out_cap, d_out_off, d_status, nullptr, ctx->geom.lane_blocks,
-                                       (hipStream_t)stream));
-        return HONU_OK;
-    }
-    if (rv == 1) {
-        HIPCHK(launch_encode_meta(ctx->geom, d_meta, d_var, d_acl, d_regions, d_payload_off, n,
-                                  d_out, out_cap, d_out_off, d_status, (hipStream_t)stream));
-        return HONU_OK;
-    }
-#endif
-    (void)rv;
     // header + tail with the ACL lists' partial end chunks (one record per
     // lane), then the lists' whole chunks (16 lanes per record)
     if (n > ctx->max_n) return HONU_E_WORKSPACE;
@@ -341,27 +304,6 @@ int32_t honu_decode_parse(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
     if (!aligned(d_rec, 16) || !aligned(d_meta, 16) || !aligned(d_info, 8))
         return arg_fail("records arena and rows must be 16-byte aligned");
     HIPCHK(hipSetDevice(ctx->device));
-    const int rv = split_rv(ctx->geom.record_variant);
-#ifdef HONU_AB
-    if (rv == 2) {
-        HIPCHK(launch_decode_parse_grp(d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
-                                       ctx->reg_inline, ctx->counts, ctx->geom.lane_blocks,
-                                       (hipStream_t)stream));
-        return HONU_OK;
-    }
-    if (rv == 3 || rv == 4) {
-        HIPCHK(launch_decode_parse_lane(d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
-                                        ctx->reg_inline, ctx->counts, ctx->geom.lane_blocks,
-                                        (hipStream_t)stream));
-        return HONU_OK;
-    }
-    if (rv == 1) {
-        HIPCHK(launch_decode_parse(ctx->geom, d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
-                                   ctx->counts, (hipStream_t)stream));
-        return HONU_OK;
-    }
-#endif
-    (void)rv;
     HIPCHK(launch_decode_parse_win(d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
                                    ctx->reg_inline, ctx->counts, ctx->geom.lane_blocks,
                                    (hipStream_t)stream));
@@ -382,22 +324,6 @@ int32_t honu_decode_tables(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n, honu
     hipStream_t s = (hipStream_t)stream;
     uint64_t *tot = d_totals ? d_totals : ctx->totals;
     HIPCHK(launch_scan(ctx->counts, n, 3, ctx->offs, tot, ctx->scan, s));
-    const int rv = split_rv(ctx->geom.record_variant);
-#ifdef HONU_AB
-    if (rv == 3) {
-        HIPCHK(launch_decode_fill_lane(d_rec, n, d_meta, d_info, ctx->scratch, ctx->counts,
-                                       ctx->offs, d_acl, acl_cap, d_regions, regions_cap, d_data,
-                                       data_cap, ctx->geom.lane_blocks, s));
-        return HONU_OK;
-    }
-    if (rv == 1) {
-        HIPCHK(launch_decode_fill(ctx->geom, d_rec, n, d_meta, d_info, ctx->scratch, ctx->counts,
-                                  ctx->offs, tot, d_acl, acl_cap, d_regions, regions_cap, d_data,
-                                  data_cap, s));
-        return HONU_OK;
-    }
-#endif
-    (void)rv;
     HIPCHK(launch_decode_fill_grp(d_rec, n, d_meta, d_info, ctx->scratch, ctx->reg_inline,
                                   ctx->counts, ctx->offs, d_acl, acl_cap, d_regions, regions_cap,
                                   d_data, data_cap, ctx->geom.lane_blocks, s));

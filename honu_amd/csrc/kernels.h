@@ -87,36 +87,17 @@ struct LaunchGeom {
     int record_variant;     // per-record kernels: 0 auto (the fastest measured form
                             // of each; honu_decode_batch single-launch from 48 K
                             // records), 5 split decode, 6 single-launch decode
-                            // at every size; A/B library only: 1 one record per
-                            // wave, 2 per group of 16 lanes, 3 per lane, 4 group
-                            // size pass and fill with lane encode and parse
+                            // at every size (the rejected one-record-per-wave /
+                            // per-group / per-lane forms 1-4: DESIGN §3)
     uint32_t *tile_map;     // sweep-form tile -> segment map (context scratch)
     uint64_t tile_map_cap;
 };
 
-hipError_t launch_encode_sizes(const LaunchGeom &g, const honu_meta *meta, uint64_t var_len,
-                               const honu_acl *acl, uint64_t acl_len, const uint32_t *reg,
-                               uint64_t reg_len, const uint64_t *payload_off, uint64_t n,
-                               uint64_t *sizes, int32_t *status, hipStream_t s);
-hipError_t launch_encode_meta(const LaunchGeom &g, const honu_meta *meta, const uint8_t *var,
-                              const honu_acl *acl, const uint32_t *reg,
-                              const uint64_t *payload_off, uint64_t n, uint8_t *out,
-                              uint64_t out_cap, const uint64_t *out_off, int32_t *status,
-                              hipStream_t s);
 hipError_t launch_encode_copy(const LaunchGeom &g, const uint8_t *payload,
                               const uint64_t *payload_off, uint64_t n, uint8_t *out,
                               uint64_t out_cap, const uint64_t *out_off, const int32_t *status,
                               hipStream_t s);
 
-hipError_t launch_decode_parse(const LaunchGeom &g, const uint8_t *rec, const uint64_t *rec_off,
-                               uint64_t n, honu_meta *meta, honu_record_info *info,
-                               DecodeScratch *scratch, uint64_t *counts, hipStream_t s);
-hipError_t launch_decode_fill(const LaunchGeom &g, const uint8_t *rec, uint64_t n,
-                              honu_meta *meta, honu_record_info *info,
-                              const DecodeScratch *scratch, const uint64_t *counts,
-                              const uint64_t *offs, const uint64_t *totals, honu_acl *acl,
-                              uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap, uint8_t *data,
-                              uint64_t data_cap, hipStream_t s);
 hipError_t launch_decode_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t n,
                               const honu_record_info *info, const DecodeScratch *scratch,
                               const uint64_t *offs, const uint64_t *totals, uint8_t *data,
@@ -125,15 +106,6 @@ hipError_t launch_decode_keys(const LaunchGeom &g, const honu_meta *meta,
                               const honu_record_info *info, uint64_t n, uint8_t *keys,
                               int32_t *key_status, hipStream_t s);
 
-hipError_t launch_decode_parse_lane(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
-                                    honu_meta *meta, honu_record_info *info,
-                                    DecodeScratch *scratch, uint32_t *reg_inline,
-                                    uint64_t *counts, int max_blocks, hipStream_t s);
-hipError_t launch_decode_fill_lane(const uint8_t *rec, uint64_t n, honu_meta *meta,
-                                   honu_record_info *info, const DecodeScratch *scratch,
-                                   const uint64_t *counts, const uint64_t *offs, honu_acl *acl,
-                                   uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap,
-                                   uint8_t *data, uint64_t data_cap, int max_blocks, hipStream_t s);
 // acl_out != null: the ACL entries are left out (positions in acl_out) for
 // launch_encode_acl_grp
 hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
@@ -143,23 +115,11 @@ hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, co
 hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uint64_t n,
                                  uint8_t *out, const int32_t *status, const uint64_t *acl_pos,
                                  int max_blocks, hipStream_t s);
-hipError_t launch_encode_sizes_lane(const honu_meta *meta, uint64_t var_len, const honu_acl *acl,
-                                    uint64_t acl_len, const uint32_t *reg, uint64_t reg_len,
-                                    const uint64_t *payload_off, uint64_t n, uint64_t *sizes,
-                                    int32_t *status, int max_blocks, hipStream_t s);
 
 hipError_t launch_encode_sizes_grp(const honu_meta *meta, uint64_t var_len, const honu_acl *acl,
                                    uint64_t acl_len, const uint32_t *reg, uint64_t reg_len,
                                    const uint64_t *payload_off, uint64_t n, uint64_t *sizes,
                                    int32_t *status, int max_blocks, hipStream_t s);
-hipError_t launch_encode_meta_grp(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
-                                  const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
-                                  uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
-                                  int32_t *status, int max_blocks, hipStream_t s);
-hipError_t launch_decode_parse_grp(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
-                                   honu_meta *meta, honu_record_info *info,
-                                   DecodeScratch *scratch, uint32_t *reg_inline, uint64_t *counts,
-                                   int max_blocks, hipStream_t s);
 hipError_t launch_decode_fill_grp(const uint8_t *rec, uint64_t n, honu_meta *meta,
                                   honu_record_info *info, const DecodeScratch *scratch,
                                   const uint32_t *reg_inline, const uint64_t *counts,

@@ -179,14 +179,8 @@ hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, co
     if (acl_out)
         hipLaunchKernelGGL(k_encode_meta_lane<true>, lane_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta,
                            var, acl, reg, payload_off, n, out, out_cap, out_off, status, acl_out);
-#ifdef HONU_AB
-    else  // the ACL entries too (record_variant 3, 4)
-        hipLaunchKernelGGL(k_encode_meta_lane<false>, lane_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta,
-                           var, acl, reg, payload_off, n, out, out_cap, out_off, status, acl_out);
-#else
     else
         return hipErrorInvalidValue;
-#endif
     return hipGetLastError();
 }
 

@@ -195,9 +195,7 @@ uint64_t honu_ctx_max_records(const honu_ctx *ctx);
  * per-record metadata kernels map records to lanes: 0 auto — the fastest
  * measured form per kernel, with honu_decode_batch running the single-launch
  * decode for batches of 48 K records or more; 5 the split decode at every
- * size; 6 the single-launch decode at every size; A/B builds add 1 one record
- * per wave, 2 one record per group of 16 lanes, 3 one record per lane, 4 lane
- * walks with group lists). Also
+ * size; 6 the single-launch decode at every size). Also
  * settable at context creation through the environment (HONU_COPY_BLOCKS,
  * HONU_RECORD_BLOCKS, HONU_LANE_BLOCKS, HONU_COPY_VARIANT, HONU_RECORD_VARIANT). */
 int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value);

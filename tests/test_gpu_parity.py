@@ -21,23 +21,17 @@ from honu_amd.metadata import META_DTYPE, normalize, pack_batch, unpack_row  # n
 from honu_amd.workload import gen_host_batch, gen_meta  # noqa: E402
 
 
-@pytest.fixture(scope="module", params=[6, 5, 1, 2, 3, 4],
-                ids=["fused", "split", "wave", "group", "lane", "lane+group"])
+@pytest.fixture(scope="module", params=[6, 5], ids=["fused", "split"])
 def codec(request):
-    """Every metadata-kernel variant: the single-launch decode (fused.hip) at
-    every batch size, and the split kernels of the default path (group size
-    pass, lane encode with group ACL lists, windowed lane parse, group fill).
-    The A/B library (make ab; HONU_LIB_PATH=honu_amd/libhonu_codec_ab.so)
-    adds one record per wave, per group of 16 lanes, per lane, and lane
-    encode/parse with the group size pass/fill; the product library refuses
-    those variants and they are skipped. (The default picks fused or split by
-    batch size; the bench pipeline and large-batch tests run it.)"""
+    """Both metadata decodes of the product library: the single-launch decode
+    (fused.hip) at every batch size, and the split kernels (group size pass,
+    lane encode with group ACL lists, windowed lane parse, group fill). The
+    default picks one by batch size; the bench pipeline and large-batch tests
+    run it."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     c = hobj.Codec(0, 1 << 18)
-    if c.lib.honu_ctx_set_param(c.ctx, b"record_variant", request.param) != 0:
-        c.close()
-        pytest.skip("A/B kernel variant: not in the product library")
+    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", request.param), "param")
     yield c
     c.close()
 
