@@ -380,11 +380,26 @@ class Bench:
         for _ in range(reps):
             once()
         e1.record(st)
+        # cold: before each timed decode an untimed 1 GiB write evicts the
+        # chunk's tails from the 256 MB Infinity Cache (back to back, a Large
+        # chunk's 66 MB of tails stay there between reps)
+        scrub = torch.empty(1 << 30, dtype=torch.uint8, device=self.dev)
+        cold = []
+        for _ in range(reps):
+            scrub.fill_(0x5A)
+            c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            c0.record(st)
+            once()
+            c1.record(st)
+            cold.append((c0, c1))
         torch.cuda.synchronize()
+        del scrub
         ncu = torch.cuda.get_device_properties(self.dev).multi_processor_count
         _lib.check(L.honu_ctx_set_param(c, b"lane_blocks", self.lane_blocks * ncu), "param")
         t = e0.elapsed_time(e1) / 1e3 / reps
-        return {"records": n, "ms": t * 1e3, "records_per_s": n / t}
+        tc = sum(x.elapsed_time(y) for x, y in cold) / 1e3 / reps
+        return {"records": n, "ms": t * 1e3, "records_per_s": n / t,
+                "cold_ms": tc * 1e3, "cold_records_per_s": n / tc}
 
 
 def copy_peak_gbs(dev, nbytes=4 << 30, reps=5):
@@ -681,6 +696,8 @@ def main(argv=None):
             "zero_copy_decode_records_per_s": zc["records_per_s"],
             "zero_copy_decode_ms_per_chunk": zc["ms"],
             "zero_copy_decode_chunk_records": zc["records"],
+            "zero_copy_decode_cold_records_per_s": zc["cold_records_per_s"],
+            "zero_copy_decode_cold_ms_per_chunk": zc["cold_ms"],
         },
         "verified": ok_all,
         "verified_scope": None if ok_all is None else Bench.VERIFIED_SCOPE,
