@@ -23,6 +23,7 @@ Prints ONE JSON line on rank 0 (see DESIGN.md for every field).
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import socket
@@ -83,6 +84,15 @@ def parse_args(argv=None):
                         "tables (split), or by chunk size as honu_decode_batch (auto)")
     p.add_argument("--copy-blocks", type=int, default=0,
                    help="workgroups per CU of the payload copy engine (0 = library default)")
+    p.add_argument("--mode", choices=["encdec", "decode"], default="encdec",
+                   help="encdec: the encode + materialising decode step (the metric); decode: "
+                        "configs[2] only, Metadata()+Data() of the whole batch from one resident "
+                        "records arena (zero copy in one call + materialising in chunks)")
+    p.add_argument("--decode-leg", choices=["both", "zero_copy", "materialising"], default="both",
+                   help="decode mode: run one leg only (PMC passes attribute a kernel's traffic "
+                        "to one leg)")
+    p.add_argument("--no-decode-legs", action="store_true",
+                   help="encdec mode: skip the whole-batch decode legs run after the timed steps")
     return p.parse_args(argv)
 
 
@@ -107,7 +117,9 @@ class Slot:
 
 
 class Bench:
-    def __init__(self, args, rank, device):
+    def __init__(self, args, rank, device, pipeline=True):
+        """pipeline=False: inputs, chunks and sizes only (no payload arena, no
+        output slots) for DecodeBench."""
         self.args = args
         self.dev = torch.device("cuda", device)
         N = args.records
@@ -143,10 +155,12 @@ class Bench:
         self.meta, self.var, self.acl, self.reg, self.off = D(meta), D(var), D(acl), D(reg), D(off)
         self.var_len, self.acl_len, self.reg_len = len(var), len(acl), len(reg)
         self.payload_bytes = int(off[N])
-        self.payload = torch.empty(self.payload_bytes + 16, dtype=torch.uint8, device=self.dev)
         s0 = torch.cuda.current_stream(self.dev).cuda_stream
-        _lib.check(self.lib.honu_gen_payload(self.codec.ctx, args.seed, self.first, N, P(self.off),
-                                             P(self.payload), s0), "gen_payload")
+        self.payload = None
+        if pipeline:
+            self.payload = torch.empty(self.payload_bytes + 16, dtype=torch.uint8, device=self.dev)
+            _lib.check(self.lib.honu_gen_payload(self.codec.ctx, args.seed, self.first, N,
+                                                 P(self.off), P(self.payload), s0), "gen_payload")
         # sizing pass (untimed): exact record bytes of every chunk
         out_off = torch.empty(8 * (C + 1), dtype=torch.uint8, device=self.dev)
         status = torch.empty(4 * C + 16, dtype=torch.uint8, device=self.dev)
@@ -165,6 +179,9 @@ class Bench:
         self.reg_cap = max(int(reg_n[a:b].sum()) for a, b in self.chunks) + 1
         self.data_cap = max(int(alloc[a:b].sum()) for a, b in self.chunks) + 16
         self.out_cap = max(self.rec_bytes) + 16
+        self.ncu = torch.cuda.get_device_properties(self.dev).multi_processor_count
+        if not pipeline:
+            return
         nslots = 1 if args.serial else 2
         self.slots = [Slot(self.dev, C, self.out_cap, self.acl_cap, self.reg_cap, self.data_cap)
                       for _ in range(nslots)]
@@ -366,6 +383,7 @@ class Bench:
                                  self.acl_len, P(self.reg), self.reg_len, P(self.payload),
                                  P(self.off) + 8 * a, n, P(sl.out), self.out_cap, P(sl.out_off),
                                  P(sl.status), st.cuda_stream), "encode")
+        self.zc_chunk = (a, b, sl)  # slot 0 holds this chunk's records from here on
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         # the decode runs alone here: lift the cap that keeps the metadata
         # kernels from crowding the copies in the pipelined step
@@ -400,6 +418,364 @@ class Bench:
         tc = sum(x.elapsed_time(y) for x, y in cold) / 1e3 / reps
         return {"records": n, "ms": t * 1e3, "records_per_s": n / t,
                 "cold_ms": tc * 1e3, "cold_records_per_s": n / tc}
+
+
+    def release(self):
+        """Free the payload arena, the output slots and the contexts (before a
+        DecodeBench reuses the device inputs)."""
+        torch.cuda.synchronize()
+        self.payload = None
+        for sl in getattr(self, "slots", []):
+            sl.codec.close()
+        self.slots = []
+        self.events = None
+        self.last = None
+        gc.collect()
+        torch.cuda.empty_cache()
+
+
+def uvarint_len(x):
+    """len(binary.PutUvarint(x)) of every element (numpy uint64)."""
+    x = np.asarray(x, np.uint64)
+    n = np.ones(x.shape, np.int64)
+    for k in range(1, 10):
+        n += x >= np.uint64(1 << (7 * k))
+    return n
+
+
+class DecodeBench:
+    """configs[2]: the reference's decode over the WHOLE batch held in one
+    records arena (object.go:66-99, the decode half of BenchmarkSerialization,
+    object_test.go:140-159).
+
+    Setup (untimed): every chunk's payload is generated into a scratch buffer
+    and the chunk is encoded into its place in one resident records arena
+    (1M Large records: ≈207 GB), with per-record digests of the source
+    payloads kept for the check. Then two legs are timed:
+      zero_copy      honu_decode_batch with no data arena over all records in
+                     ONE call: Metadata() rows, record info (Data() subslices of
+                     the arena) and the ACL / region tables;
+      materialising  the same decode with Data() copied into a packed data
+                     arena, chunk by chunk (the data arena of 1M Large records
+                     does not fit beside the records), metadata decode of chunk
+                     k+1 on one stream beside the payload copy of chunk k on
+                     another, two data slots.
+    Rows and record info of both legs go to whole-batch arrays; every row,
+    table entry and payload is checked after the timed reps."""
+
+    def __init__(self, bench):
+        self.b = b = bench
+        self.args = bench.args
+        self.dev = b.dev
+        self.lib = L = b.lib
+        N, C = b.N, b.C
+        dev = self.dev
+        E = lambda nb: torch.empty(int(nb), dtype=torch.uint8, device=dev)  # noqa: E731
+        self.codec = Codec(dev.index, max_records=N)
+        c = self.codec.ctx
+        st = torch.cuda.current_stream(dev)
+        s = st.cuda_stream
+        # global record offsets: sizes of every record, one scan
+        self.rec_off = E(8 * (N + 1))
+        self.status = E(4 * N + 16)
+        _lib.check(L.honu_encode_sizes(c, P(b.meta), b.var_len, P(b.acl), b.acl_len, P(b.reg),
+                                       b.reg_len, P(b.off), N, P(self.rec_off), P(self.status), s),
+                   "sizes")
+        _lib.check(L.honu_exclusive_scan(c, P(self.rec_off), N, P(self.rec_off), s), "scan")
+        ro = self.rec_off.view(torch.int64)
+        self.total = int(ro[N].item())
+        self.arena = E(self.total + 16)
+        self.dig_src = E(8 * N)
+        scratch = E(max(b.chunk_payload) + 16)
+        host_off = b.host_off
+        for a, e in b.chunks:  # payload of chunk -> scratch -> encoded into the arena
+            n = e - a
+            base = P(scratch) - int(host_off[a])  # payload offsets are global
+            _lib.check(L.honu_gen_payload(c, self.args.seed, b.first + a, n, P(b.off) + 8 * a, base,
+                                          s), "gen_payload")
+            _lib.check(L.honu_digest_records(c, base, P(b.off) + 8 * a, 0, n,
+                                             P(self.dig_src) + 8 * a, s), "digest")
+            _lib.check(L.honu_encode(c, P(b.meta) + 352 * a, P(b.var), b.var_len, P(b.acl),
+                                     b.acl_len, P(b.reg), b.reg_len, base, P(b.off) + 8 * a, n,
+                                     P(self.arena), self.total + 16, P(self.rec_off) + 8 * a,
+                                     P(self.status) + 4 * a, s), "encode")
+            st.synchronize()
+        del scratch
+        self.encode_ok = bool((self.status[: 4 * N].view(torch.int32) == 0).all())
+        torch.cuda.empty_cache()
+        # algorithmic bytes (SURVEY §8d): per record the offsets pair, the
+        # header, the Metadata tail; out the row, the record info, the tables
+        rlen = np.diff(ro.cpu().numpy())
+        plen = np.diff(host_off.astype(np.int64))
+        hdr = 1 + uvarint_len(plen)
+        self.tail_bytes = int((rlen - hdr - plen).sum())
+        self.hdr_bytes = int(hdr.sum())
+        hm = b.host_meta
+        self.nacl = int(hm["acl_count"].astype(np.int64).sum())
+        self.nreg = int(hm["regions_count"].astype(np.int64).sum())
+        self.meta_bytes = (8 * N + self.hdr_bytes + self.tail_bytes + 352 * N + 32 * N +
+                           20 * self.nacl + 4 * self.nreg)
+        self.payload_bytes = int(plen.sum())
+        # whole-batch outputs
+        self.dmeta, self.dinfo = E(352 * N), E(32 * N)
+        self.acl_cap, self.reg_cap = self.nacl + 1, self.nreg + 1
+        self.dacl, self.dreg = E(20 * self.acl_cap), E(4 * self.reg_cap)
+        self.totals = E(32)
+        # materialising leg: two data slots of one chunk each
+        self.slots = []
+        for _ in range(2):
+            sl = Slot.__new__(Slot)
+            sl.codec = Codec(dev.index, max_records=C)
+            sl.dacl, sl.dreg = E(20 * b.acl_cap), E(4 * b.reg_cap)
+            sl.data, sl.totals = E(b.data_cap), E(32)
+            sl.free = None
+            self.slots.append(sl)
+        self.sm = torch.cuda.Stream(dev)
+        self.sc = torch.cuda.Stream(dev, priority=-1)
+        self.sv = torch.cuda.Stream(dev)
+        torch.cuda.synchronize()
+
+    # -- zero copy, whole batch ------------------------------------------------
+    def _zero_copy_once(self, s):
+        b, L = self.b, self.lib
+        _lib.check(L.honu_decode_batch(self.codec.ctx, P(self.arena), P(self.rec_off), b.N,
+                                       P(self.dmeta), P(self.dinfo), P(self.dacl), self.acl_cap,
+                                       P(self.dreg), self.reg_cap, 0, 0, P(self.totals), s),
+                   "decode_batch")
+
+    def zero_copy(self, reps):
+        st = torch.cuda.current_stream(self.dev)
+        self._zero_copy_once(st.cuda_stream)
+        ev = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            self._zero_copy_once(st.cuda_stream)
+            e1.record(st)
+            ev.append((e0, e1))
+        torch.cuda.synchronize()
+        ms = [x.elapsed_time(y) for x, y in ev]
+        t = sum(ms) / len(ms) / 1e3
+        N = self.b.N
+        gbs = self.meta_bytes / t / 1e9
+        return {
+            "records": N,
+            "reps": reps,
+            "ms": t * 1e3,
+            "ms_min": min(ms),
+            "records_per_s": N / t,
+            "calls": "honu_decode_batch(data arena NULL) over all records, one call",
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_decode_fused",
+                "achieved": gbs,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": gbs / HBM_PEAK_GBS,
+                "traffic": pmc_traffic(self.workload("zero_copy"), "k_decode_fused"),
+                "avg_launch_ms": t * 1e3,
+                "algorithmic_bytes_per_launch": self.meta_bytes,
+                "algorithmic_bytes": "8 (offsets) + header + Metadata tail read; 352 row + 32 info "
+                                     "+ 20 per ACL entry + 4 per region written, per record",
+            },
+        }
+
+    def check_zero_copy(self):
+        """Every row / table entry against its source row; every Data() subslice's
+        digest against its source payload's."""
+        b, L, N = self.b, self.lib, self.b.N
+        torch.cuda.synchronize()
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        c = self.codec.ctx
+        mism = torch.empty(4 * N, dtype=torch.uint8, device=self.dev)
+        _lib.check(L.honu_verify_decoded(c, P(b.meta), P(b.var), P(b.acl), P(b.reg), P(b.off),
+                                         P(self.arena), P(self.dmeta), P(self.dinfo), P(self.dacl),
+                                         P(self.dreg), N, P(mism), s), "verify")
+        info = self.dinfo.view(torch.int64).view(N, 4)
+        doff, dlen = info[:, 0].contiguous(), info[:, 1].contiguous()
+        dd = torch.empty(8 * N, dtype=torch.uint8, device=self.dev)
+        _lib.check(L.honu_digest_records(c, P(self.arena), P(doff), P(dlen), N, P(dd), s), "digest")
+        ok = int(torch.count_nonzero(mism.view(torch.int32))) == 0 and torch.equal(dd, self.dig_src)
+        return bool(ok) and self.encode_ok
+
+    # -- materialising, chunk by chunk ---------------------------------------------
+    def _issue(self, k, a, e, timed):
+        b, L = self.b, self.lib
+        n = e - a
+        sl = self.slots[k % 2]
+        c = sl.codec.ctx
+        sm, sc = self.sm, self.sc
+        if sl.free is not None:
+            sm.wait_event(sl.free)
+        ms = sm.cuda_stream
+        ro = P(self.rec_off) + 8 * a
+        if n >= FUSED_DECODE_MIN:  # honu_decode_batch's own choice of kernels
+            _lib.check(L.honu_decode_records(c, P(self.arena), ro, n, P(self.dmeta) + 352 * a,
+                                             P(self.dinfo) + 32 * a, P(sl.dacl), b.acl_cap,
+                                             P(sl.dreg), b.reg_cap, 1, b.data_cap, P(sl.totals), ms),
+                       "decode_records")
+        else:
+            _lib.check(L.honu_decode_parse(c, P(self.arena), ro, n, P(self.dmeta) + 352 * a,
+                                           P(self.dinfo) + 32 * a, ms), "decode_parse")
+            _lib.check(L.honu_decode_tables(c, P(self.arena), n, P(self.dmeta) + 352 * a,
+                                            P(self.dinfo) + 32 * a, P(sl.dacl), b.acl_cap,
+                                            P(sl.dreg), b.reg_cap, P(sl.data), b.data_cap,
+                                            P(sl.totals), ms), "decode_tables")
+        ev = torch.cuda.Event()
+        ev.record(sm)
+        sc.wait_event(ev)
+        e0 = torch.cuda.Event(enable_timing=True) if timed else None
+        e1 = torch.cuda.Event(enable_timing=True) if timed else None
+        if timed:
+            e0.record(sc)
+        _lib.check(L.honu_decode_payloads(c, P(self.arena), n, P(self.dinfo) + 32 * a, P(sl.data),
+                                          P(sl.totals), sc.cuda_stream), "decode_payloads")
+        if timed:
+            e1.record(sc)
+            self.events.append((a, e, e0, e1))
+        sl.free = torch.cuda.Event()
+        sl.free.record(sc)
+        return sl
+
+    def materialise_pass(self, timed=False, check=None):
+        ok, pending = True, None
+        for k, (a, e) in enumerate(self.b.chunks):
+            sl = self._issue(k, a, e, timed)
+            if check is not None:
+                if pending is not None:
+                    ok &= self._check(check, pending)
+                pending = (a, e, sl)
+        if pending is not None:
+            ok &= self._check(check, pending)
+        cur = torch.cuda.current_stream(self.dev)
+        cur.wait_stream(self.sc)
+        cur.wait_stream(self.sm)
+        return ok
+
+    def _check(self, check, pending):
+        a, e, sl = pending
+        sl.free.synchronize()
+        with torch.cuda.stream(self.sv):
+            return bool(check(a, e, sl))
+
+    def _check_chunk(self, a, e, sl):
+        b, L = self.b, self.lib
+        n = e - a
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        c = sl.codec.ctx
+        mism = torch.empty(4 * n, dtype=torch.uint8, device=self.dev)
+        _lib.check(L.honu_verify_decoded(c, P(b.meta) + 352 * a, P(b.var), P(b.acl), P(b.reg),
+                                         P(b.off) + 8 * a, P(self.arena), P(self.dmeta) + 352 * a,
+                                         P(self.dinfo) + 32 * a, P(sl.dacl), P(sl.dreg), n, P(mism),
+                                         s), "verify")
+        info = self.dinfo[32 * a: 32 * e].view(torch.int64).view(n, 4)
+        doff, dlen = info[:, 0].contiguous(), info[:, 1].contiguous()
+        dd = torch.empty(8 * n, dtype=torch.uint8, device=self.dev)
+        _lib.check(L.honu_digest_records(c, P(sl.data), P(doff), P(dlen), n, P(dd), s), "digest")
+        ok = int(torch.count_nonzero(mism.view(torch.int32))) == 0
+        ok &= torch.equal(dd, self.dig_src[8 * a: 8 * e])
+        torch.cuda.current_stream(self.dev).synchronize()
+        return bool(ok)
+
+    def materialising(self, steps, warmup):
+        for _ in range(warmup):
+            self.materialise_pass()
+        torch.cuda.synchronize()
+        self.events = []
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.materialise_pass(timed=True)
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / steps
+        copy_ms = [x.elapsed_time(y) for (_, _, x, y) in self.events]
+        chunk_pay = {a: p for (a, _), p in zip(self.b.chunks, self.b.chunk_payload)}
+        copy_bytes = [2 * chunk_pay[a] for (a, _, _, _) in self.events]
+        cg = sum(copy_bytes) / (sum(copy_ms) / 1e3) / 1e9
+        step_bytes = self.meta_bytes + 2 * self.payload_bytes
+        return {
+            "records": self.b.N,
+            "chunks": len(self.b.chunks),
+            "steps": steps,
+            "ms_per_pass": el * 1e3,
+            "gib_s": self.total / el / 2**30,
+            "records_per_s": self.b.N / el,
+            "hbm_gbs_algorithmic": step_bytes / el / 1e9,
+            "frac_of_spec_whole_pass": step_bytes / el / 1e9 / HBM_PEAK_GBS,
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_copy_segments<honu::DecodeSegments>",
+                "achieved": cg,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": cg / HBM_PEAK_GBS,
+                "traffic": pmc_traffic(self.workload("materialising"),
+                                       "k_copy_segments<honu::DecodeSegments"),
+                "launches": len(copy_ms),
+                "avg_launch_ms": sum(copy_ms) / len(copy_ms),
+                "algorithmic_bytes_per_launch": sum(copy_bytes) / len(copy_bytes),
+            },
+        }
+
+    def workload(self, leg):
+        b = self.b
+        return (f"{b.N} {self.args.shape} records per GPU: decode (Object.Metadata + Object.Data) "
+                f"of one resident records arena, {leg}")
+
+    def run(self, steps, warmup):
+        leg = getattr(self.args, "decode_leg", "both")
+        zc = mat = None
+        zc_ok = mat_ok = True
+        if leg in ("both", "zero_copy"):
+            zc = self.zero_copy(max(3, steps))
+            zc_ok = None if self.args.no_verify else self.check_zero_copy()
+        if leg in ("both", "materialising"):
+            mat = self.materialising(steps, warmup)
+            mat_ok = None if self.args.no_verify else bool(
+                self.materialise_pass(check=self._check_chunk))
+        name = {"both": "zero copy (one call) + materialising (chunked)", "zero_copy": "zero_copy",
+                "materialising": "materialising"}[leg]
+        return {
+            "workload": self.workload(name),
+            "records_arena_bytes": self.total,
+            "payload_bytes": self.payload_bytes,
+            "metadata_tail_bytes": self.tail_bytes,
+            "acl_entries": self.nacl,
+            "regions": self.nreg,
+            "zero_copy": zc,
+            "materialising": mat,
+            "verified": None if self.args.no_verify else bool(zc_ok and mat_ok),
+            "verified_scope": None if self.args.no_verify else (
+                "every record: encode status; both legs: every decoded row byte, span, ACL entry "
+                "and region against its source row (honu_verify_decoded), every Data() subslice "
+                "(zero copy) / materialised payload digest against its source's"),
+        }
+
+    def release(self):
+        torch.cuda.synchronize()
+        for sl in self.slots:
+            sl.codec.close()
+        self.codec.close()
+        self.slots = []
+        self.arena = None
+        gc.collect()
+        torch.cuda.empty_cache()
+
+
+# honu_decode_batch's crossover to the single-launch decode (api.hip FUSED_DECODE_MIN_RECORDS)
+FUSED_DECODE_MIN = 48 << 10
+
+
+def pmc_traffic(workload, kernel_prefix):
+    """HBM bytes per launch of kernel from the PMC passes of this same command
+    (profiles/pmc_traffic.json, tools/pmc_traffic.py), or None."""
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(tpath):
+        return None
+    pm = json.load(open(tpath)).get("workloads", {}).get(workload, {})
+    for k, v in pm.get("kernels", {}).items():
+        if k.startswith("void honu::" + kernel_prefix) or k.startswith("honu::" + kernel_prefix):
+            return v["traffic_per_launch"]
+    return None
 
 
 def copy_peak_gbs(dev, nbytes=4 << 30, reps=5):
@@ -447,21 +823,27 @@ def cpu_baseline(args):
     def run(ranges, seconds):
         done = [0] * len(ranges)
         nbytes = [0] * len(ranges)
-        stop = time.perf_counter() + seconds
+        # every thread's output arrays are allocated and faulted in once, before
+        # the clock starts (oracle.CycleWorkspace), so the loop times the codec
+        wss = [oracle.CycleWorkspace(HostBatch(meta[a:b], var, acl, reg, payload, off[a:b + 1]))
+               for a, b in ranges]
+        start = threading.Barrier(len(ranges) + 1)
+        stop = [0.0]
 
-        def work(k, a, b):
-            hb = HostBatch(meta[a:b], var, acl, reg, payload, off[a:b + 1])
+        def work(k, b_minus_a):
+            ws = wss[k]
+            start.wait()
             while True:
-                out, ooff, _ = oracle.marshal_batch(hb)
-                oracle.decode_batch(out, ooff, materialize=True)
-                nbytes[k] += int(ooff[-1])
-                done[k] += b - a
-                if time.perf_counter() >= stop:
+                nbytes[k] += ws.cycle()
+                done[k] += b_minus_a
+                if time.perf_counter() >= stop[0]:
                     break
-        t0 = time.perf_counter()
-        ths = [threading.Thread(target=work, args=(k, a, b)) for k, (a, b) in enumerate(ranges)]
+        ths = [threading.Thread(target=work, args=(k, b - a)) for k, (a, b) in enumerate(ranges)]
         for t in ths:
             t.start()
+        t0 = time.perf_counter()
+        stop[0] = t0 + seconds
+        start.wait()
         for t in ths:
             t.join()
         el = time.perf_counter() - t0
@@ -485,7 +867,7 @@ def cpu_baseline(args):
         "value_1core": one_gib,
         "records_per_s_1core": one_rps,
         "sample": f"{n} {args.shape} records (seed {args.seed}) encoded + decoded (materialising) "
-                  f"by the C oracle, cycled for {one_s:.1f} s on 1 thread and {all_s:.1f} s on "
+                  f"by the C oracle into output arrays allocated once per thread, cycled for {one_s:.1f} s on 1 thread and {all_s:.1f} s on "
                   f"{T} threads (record ranges per thread), {model}; no Go toolchain on the box, "
                   "so the Go reference itself cannot be timed",
     }
@@ -570,12 +952,178 @@ def main(argv=None):
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    bench = Bench(args, rank, local)
-
     def barrier():
         if dist is not None:
             dist.barrier()
 
+    gather_max, all_ok = make_reducers(dist, world, torch.device("cuda", local))
+
+    if args.mode == "decode":
+        result = decode_mode(args, rank, local, world, dist, barrier, gather_max, all_ok)
+    else:
+        result = encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok)
+    if result is not None and rank == 0:
+        if not args.no_cpu_baseline:  # rank 0 only, after every collective leg
+            result["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def make_reducers(dist, world, device):
+    """(gather_max, all_ok) over the ranks of the default group (identity
+    without one): gather_max(x) -> (max over ranks, every rank's x);
+    all_ok(flag) -> AND over ranks (None stays None)."""
+    def gather_max(x):
+        if dist is None:
+            return x, [x]
+        t = torch.tensor([x], dtype=torch.float64, device=device)
+        g = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(g, t)
+        vals = [float(v.item()) for v in g]
+        return max(vals), vals
+
+    def all_ok(flag):
+        if flag is None or dist is None:
+            return flag
+        v = torch.tensor([1 if flag else 0], device=device)
+        dist.all_reduce(v, op=dist.ReduceOp.MIN)
+        return bool(v.item())
+    return gather_max, all_ok
+
+
+def decode_legs(bench, args, world, barrier, gather_max, all_ok):
+    """The whole-batch decode legs (DecodeBench) of this rank's shard, timed
+    between barriers; aggregates over ranks."""
+    db = DecodeBench(bench)
+    barrier()
+    res = db.run(args.steps, args.warmup)
+    db.release()
+    res["verified"] = all_ok(res["verified"])
+    agg = {"ranks": world}
+    if res["zero_copy"] is not None:
+        zc_ms, zc_all = gather_max(res["zero_copy"]["ms"])
+        agg.update(zero_copy_ms_max=zc_ms, zero_copy_records_per_s=world * bench.N / (zc_ms / 1e3),
+                   per_rank_zero_copy_ms=zc_all)
+    if res["materialising"] is not None:
+        mat_ms, mat_all = gather_max(res["materialising"]["ms_per_pass"])
+        agg.update(materialising_ms_max=mat_ms,
+                   materialising_gib_s=world * db.total / (mat_ms / 1e3) / 2**30,
+                   per_rank_materialising_ms=mat_all)
+    res["all_ranks"] = agg
+    return res
+
+
+def host_path_leg(bench, args, local, world, gather_max, all_ok, measure=None):
+    """SURVEY §8d/§8e host path on every rank at once: pinned H2D -> codec ->
+    D2H of a ~4 GiB sample of the rank's own records (tools/host_path.py
+    measure); aggregate = all ranks' bytes / the slowest rank's time."""
+    if measure is None:
+        from tools.host_path import measure
+    avg = bench.total_rec_bytes / bench.N
+    n = int(max(256, min(bench.N, (4 << 30) // max(1, int(avg)))))
+    chunk = int(max(256, n // 8))  # ~512 MiB per transfer (PCIe-rate chunks)
+    r = measure(args.shape, n, chunk, reps=2, device=local, first=bench.first)
+    enc_s, _ = gather_max(r["encode_s"])
+    dec_s, _ = gather_max(r["decode_s"])
+    r["rows_match"] = all_ok(r["rows_match"])
+    r["all_ranks"] = {
+        "ranks": world,
+        "encode_host_path_gbs": world * r["record_bytes"] / enc_s / 1e9,
+        "decode_host_path_gbs": world * r["record_bytes"] / dec_s / 1e9,
+    }
+    return r
+
+
+def scatter_leg(arena, off, dist, world, all_ok, decode_check, sync=None):
+    """N > 1 (north_star: RCCL over xGMI only as a plain scatter of
+    sub-batches): rank 0's encoded records (arena, off[n+1] int64; None on the
+    other ranks) are sent as byte-balanced sub-batches to every rank in one
+    group of point-to-point sends (honu_amd.shard.scatter_records: RCCL
+    isend/irecv under nccl, gloo on CPU); every rank checks what arrived with
+    decode_check(arena, off, n) -> bool. Outside the codec's timed region."""
+    from honu_amd.shard import scatter_records
+    sync = sync or (lambda: None)
+    times = []
+    for _ in range(2):
+        dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        mine, moff, first, cnt, sent = scatter_records(arena, off, src=0)
+        sync()
+        dist.barrier()
+        times.append(time.perf_counter() - t0)
+    ok = all_ok(bool(decode_check(mine, moff, cnt)))
+    sent_t = torch.tensor([sent], dtype=torch.int64, device=moff.device)
+    dist.all_reduce(sent_t, op=dist.ReduceOp.MAX)
+    sent = int(sent_t.item())
+    t = min(times)
+    return {"bytes_sent_by_rank0": sent, "scatter_ms": t * 1e3, "scatter_gbs": sent / t / 1e9,
+            "per_link_gbs": sent / t / 1e9 / max(1, world - 1), "verified": ok,
+            "how": "point-to-point sends batched in one group (batch_isend_irecv) from rank 0, "
+                   "byte-balanced contiguous sub-batches, then a zero-copy parse on every rank "
+                   "with every status checked"}
+
+
+def gpu_parse_check(local):
+    """decode_check for scatter_leg: Metadata() + Data() (zero-copy parse) of
+    the received records on this rank's GPU; True when every status is OK."""
+    def check(mine, moff, cnt):
+        c = Codec(local, max(cnt, 1))
+        dev = torch.device("cuda", local)
+        rows = torch.empty(352 * max(cnt, 1), dtype=torch.uint8, device=dev)
+        info = torch.empty(32 * max(cnt, 1), dtype=torch.uint8, device=dev)
+        s = torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(c.lib.honu_decode_parse(c.ctx, P(mine), P(moff), cnt, P(rows), P(info), s),
+                   "parse")
+        torch.cuda.synchronize()
+        st32 = info[: 32 * cnt].view(torch.int64).view(cnt, 4)[:, 2].contiguous().view(torch.int32)
+        ok = bool((st32 == 0).all())
+        c.close()
+        return ok
+    return check
+
+
+def decode_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
+    """configs[2] alone: the whole-batch decode legs; the line's value is the
+    materialising decode rate (records arena bytes / s, all ranks)."""
+    bench = Bench(args, rank, local, pipeline=False)
+    res = decode_legs(bench, args, world, barrier, gather_max, all_ok)
+    if rank != 0:
+        return None
+    agg = res["all_ranks"]
+    mat, zc = res["materialising"], res["zero_copy"]
+    if mat is None:  # zero-copy leg alone: records arena bytes / s of Metadata()+Data()
+        ms = agg["zero_copy_ms_max"]
+        value, roof = world * res["records_arena_bytes"] / (ms / 1e3) / 2**30, zc["roofline"]
+    else:
+        ms = agg["materialising_ms_max"]
+        value, roof = agg["materialising_gib_s"], mat["roofline"]
+    return {
+        "metric": METRIC,
+        "value": value,
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: seeded generator mirroring object_test.go:195-386, payload bytes "
+                "generated on device",
+        "config": {"workload": res["workload"], "records_per_gpu": bench.N, "shape": args.shape,
+                   "parallelism": f"dp{world} (records sharded, no data-path collective)"},
+        "records_per_s": world * bench.N / (ms / 1e3),
+        "roofline": roof,
+        "decode": res,
+        "verified": res["verified"],
+    }
+
+
+def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
+    bench = Bench(args, rank, local)
     for _ in range(args.warmup):
         bench.step()
     torch.cuda.synchronize()
@@ -594,11 +1142,7 @@ def main(argv=None):
     ranks, backend = 1, None
     if dist is not None:
         ranks, backend = dist.get_world_size(), dist.get_backend()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=bench.dev)
-        gathered = [torch.zeros_like(t) for _ in range(ranks)]
-        dist.all_gather(gathered, t)
-        per_rank_s = [float(x.item()) for x in gathered]
-        elapsed = max(per_rank_s)
+        elapsed, per_rank_s = gather_max(elapsed)
         tt = torch.tensor(tot, dtype=torch.int64, device=bench.dev)
         dist.all_reduce(tt, op=dist.ReduceOp.SUM)
         tot = [int(x) for x in tt.tolist()]
@@ -611,33 +1155,37 @@ def main(argv=None):
     dec_gbs = sum(enc_bytes) / (sum(dec_ms) / 1e3) / 1e9
     verified = None if args.no_verify else bench.verify()
     zc = bench.zero_copy_decode()
-    ok_all = verified
-    if dist is not None and verified is not None:
-        v = torch.tensor([1 if verified else 0], device=bench.dev)
-        dist.all_reduce(v, op=dist.ReduceOp.MIN)
-        ok_all = bool(v.item())
-
+    ok_all = all_ok(verified)
+    peak_meas = copy_peak_gbs(bench.dev)
+    # the legs after the timed steps: none of them changes the numbers above
+    bench.payload = None  # the scatter leg keeps the output slots, nothing else
+    gc.collect()
+    torch.cuda.empty_cache()
+    scatter = None
+    if dist is not None:
+        arena = off = None
+        if rank == 0:  # the chunk zero_copy_decode left encoded in slot 0
+            a, b, sl = bench.zc_chunk
+            off = sl.out_off.view(torch.int64)[: b - a + 1]
+            arena = sl.out[: int(off[b - a].item())]
+        scatter = scatter_leg(arena, off, dist, world, all_ok, gpu_parse_check(local),
+                              torch.cuda.synchronize)
+    bench.release()
+    host_path = host_path_leg(bench, args, local, world, gather_max, all_ok)
+    decode = None if args.no_decode_legs else decode_legs(bench, args, world, barrier, gather_max,
+                                                          all_ok)
     if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
-        return
+        return None
     step_s = elapsed / args.steps
     total_bytes, total_records = tot
     launches = len(dec_ms)
     dom_ms, dom_gbs, dom_name = (sum(dec_ms), dec_gbs, "k_copy_segments<honu::DecodeSegments>")
     if sum(enc_ms) > sum(dec_ms):
         dom_ms, dom_gbs, dom_name = (sum(enc_ms), enc_gbs, "k_copy_segments<honu::EncodeSegments>")
-    peak_meas = copy_peak_gbs(bench.dev)
     workload = (f"{bench.N} {args.shape} records per GPU: encode (object.Marshal) + "
                 "materialising decode (Object.Metadata + Object.Data)")
-    traffic, traffic_src = None, None
-    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tpath):  # PMC passes of this same command (tools/pmc_traffic.py)
-        pm = json.load(open(tpath)).get("workloads", {}).get(workload, {})
-        kn = dom_name.split("<")[0] + "<" + dom_name.split("<")[1].split(">")[0]
-        for k, v in pm.get("kernels", {}).items():
-            if k.startswith("void honu::" + kn):
-                traffic, traffic_src = v["traffic_per_launch"], "profiles/pmc_traffic.json"
+    kn = dom_name.split(">")[0]
+    traffic = pmc_traffic(workload, kn)  # PMC passes of this same command (tools/pmc_traffic.py)
     result = {
         "metric": METRIC,
         "value": total_bytes / step_s / 2**30,
@@ -681,7 +1229,7 @@ def main(argv=None):
             "unit": "GB/s",
             "frac": dom_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
-            "traffic_source": traffic_src,
+            "traffic_source": "profiles/pmc_traffic.json" if traffic else None,
             "launches": launches,
             "avg_launch_ms": dom_ms / launches,
             "algorithmic_bytes_per_launch": sum(enc_bytes) / launches,
@@ -701,12 +1249,11 @@ def main(argv=None):
         },
         "verified": ok_all,
         "verified_scope": None if ok_all is None else Bench.VERIFIED_SCOPE,
+        "decode": decode,
+        "host_path": host_path,
+        "scatter": scatter,
     }
-    if world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args)
-    print(json.dumps(result), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    return result
 
 
 if __name__ == "__main__":

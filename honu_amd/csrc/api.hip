@@ -28,6 +28,7 @@ struct honu_ctx {
     LbState *lb_dec;
     uint64_t *lb_dec_status;
     uint64_t lb_dec_words;
+    uint64_t lb_bytes;       // the look-back blocks + status words, from lb_dec
     ScanState scan;          // look-back state of the one-launch scans (scan.hip)
 };
 
@@ -172,14 +173,29 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->scan.status = c->lb_dec_status + c->lb_dec_words;
     c->scan.words = scan_words;
     c->scan.max_blocks = 4 * prop.multiProcessorCount;
-    // clean look-back state: epoch 0 with no published tile
-    if (hipMemset(c->lb_dec, 0, lb_bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    c->lb_bytes = lb_bytes;
+    // clean look-back state: epoch 0 with no published tile. On a stream of
+    // the call's own, so work other contexts have in flight keeps running.
+    hipStream_t s = nullptr;
+    bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipMemsetAsync(c->lb_dec, 0, lb_bytes, s) == hipSuccess;
+    ok = ok && hipStreamSynchronize(s) == hipSuccess;
+    if (s) (void)hipStreamDestroy(s);
+    if (!ok) {
         (void)hipFree(c->ws);
         free(c);
         *err = HONU_E_HIP;
         return nullptr;
     }
     return c;
+}
+
+int32_t honu_ctx_reset(honu_ctx *ctx, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemsetAsync(ctx->lb_dec, 0, ctx->lb_bytes, (hipStream_t)stream));
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    return HONU_OK;
 }
 
 void honu_ctx_destroy(honu_ctx *ctx) {

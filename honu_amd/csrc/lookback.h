@@ -148,9 +148,15 @@ HONU_DEV void lb_finish(LbState *s, uint64_t *status, uint64_t status_words, uin
 }
 
 // Static tiles instead of tickets, for a launch whose tiles all fit its
-// resident waves (one tile per wave, tile = the wave's global index: every
-// predecessor a wave waits on belongs to a wave that is or will be resident,
-// as the whole grid fits the chip). Saves the launch-time burst of ticket
+// resident waves (one tile per wave, tile = the wave's global index). A wave
+// waits only on lower-numbered tiles, i.e. on waves of its own or of
+// lower-numbered workgroups. Forward progress RELIES ON IN-ORDER WORKGROUP
+// DISPATCH (the assumption CUB's blockIdx-tiled decoupled look-back makes):
+// the dispatcher launches a grid's workgroups in blockIdx order, so every
+// workgroup a waiting wave depends on was dispatched before it and is resident
+// or finished, also when kernels of other streams hold part of the chip and
+// this grid is not resident all at once (tests/test_lookback.py runs the
+// decode in this mode beside a copy that fills the CUs). Saves the launch-time burst of ticket
 // atomics on one address (~20 us for 2048 waves). The last workgroup to
 // finish (one atomic per workgroup) resets the count and advances the epoch;
 // on a wrap of the epoch it clears the status array first. Called by every

@@ -10,7 +10,7 @@ UnmarshalSystem decodes obj[1 : len-1] without checking the version byte.
 from __future__ import annotations
 
 import copy
-from dataclasses import dataclass, field
+from dataclasses import dataclass, field, fields
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -304,8 +304,11 @@ def UnmarshalSystem(obj: bytes) -> Collection:
 def Unmarshal(raw: bytes, c: Optional[Collection] = None) -> Collection:
     """lani.Unmarshal(raw, c) with c a *metadata.Collection (lani/lani.go:29-33):
     Collection.Decode from byte 0 of raw, as pkg/store calls it on raw bbolt
-    values (store.go:155, :367). c=None is store.go:155's nil pointer, on
-    which the reference panics (collection.go:242 assigns through it)."""
+    values (store.go:155, :367). Decodes INTO c, as the Go decoder assigns
+    every field of *c (collection.go:242-356), and returns c. c=None is
+    store.go:155's nil pointer, on which the reference panics. On an error c is
+    left as it was (Go may have assigned a prefix of the fields; callers
+    discard c on error)."""
     from .object import _ERRORS, GoPanic, HonuCodecError
     if c is None:
         raise GoPanic("Collection.Decode on a nil *Collection (store.go:155)")
@@ -314,4 +317,7 @@ def Unmarshal(raw: bytes, c: Optional[Collection] = None) -> Collection:
                                                      headless=True)
     if st[0]:
         raise _ERRORS.get(int(st[0]), HonuCodecError)(f"status {int(st[0])}")
-    return unpack_collection(rows[0], rec, acl, reg, idx)
+    out = unpack_collection(rows[0], rec, acl, reg, idx)
+    for f in fields(out):
+        setattr(c, f.name, getattr(out, f.name))
+    return c

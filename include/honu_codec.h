@@ -186,6 +186,16 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err);
 void honu_ctx_destroy(honu_ctx *ctx);
 uint64_t honu_ctx_max_records(const honu_ctx *ctx);
 
+/* The single-launch decode and the one-launch scans keep decoupled look-back
+ * state in the context (a tile ticket, a finished-workgroup count and a launch
+ * epoch) that each launch leaves clean for the next, so nothing is cleared
+ * per call and the calls replay from a captured hipGraph. A launch that did
+ * not run to completion (its stream was torn down, the device reset) can leave
+ * it dirty: a context that saw a HIP error (HONU_E_HIP) must be reset with
+ * honu_ctx_reset, on a stream with no other work of this context in flight,
+ * before its next decode or scan (it returns when the reset is done). */
+int32_t honu_ctx_reset(honu_ctx *ctx, void *stream);
+
 /* Launch-geometry knobs (defaults suit MI355X): "copy_blocks" (workgroups of
  * the payload copy kernel, default 2 per CU), "record_blocks" (cap on
  * workgroups of the one-wave-per-record kernels, default 8 per CU),

@@ -130,6 +130,51 @@ def decode_batch(rec: np.ndarray, rec_off: np.ndarray, materialize: bool = False
             None if data is None else data[: int(totals[2])], totals)
 
 
+class CycleWorkspace:
+    """Output arrays of one marshal + materialising decode of a HostBatch,
+    allocated once (tables sized by the batch's ACL entry and region counts,
+    the data arena by its payload bytes) so that a timing loop measures the
+    codec, not allocation and page faults. cycle() re-encodes the batch into
+    `out` and decodes it into the tables; returns the encoded bytes."""
+
+    def __init__(self, hb):
+        from honu_amd.metadata import ACL_DTYPE, INFO_DTYPE, META_DTYPE
+        self.hb = hb
+        self.lib = load()
+        n = len(hb.meta)
+        self.n = n
+        self.out_off = np.zeros(n + 1, np.uint64)
+        self.status = np.zeros(max(n, 1), np.int32)
+        self._marshal(None, 0)  # size pass: out_off
+        self.total = int(self.out_off[n])
+        self.out = np.zeros(max(self.total, 1), np.uint8)
+        self.meta = np.zeros(max(n, 1), META_DTYPE)
+        self.info = np.zeros(max(n, 1), INFO_DTYPE)
+        nacl = int(hb.meta["acl_count"].astype(np.int64).sum()) if n else 0
+        nreg = int(hb.meta["regions_count"].astype(np.int64).sum()) if n else 0
+        self.acl = np.zeros(nacl + 1, ACL_DTYPE)
+        self.reg = np.zeros(nreg + 1, np.uint32)
+        pay = np.diff(np.asarray(hb.payload_off, np.int64)) if n else np.zeros(0, np.int64)
+        self.data = np.zeros(int(((pay + 15) // 16 * 16).sum()) + 16, np.uint8)
+        self.totals = np.zeros(3, np.uint64)
+        for a in (self.out, self.meta, self.info, self.acl, self.reg, self.data):
+            a.view(np.uint8).reshape(-1)[::4096] = 0  # fault the pages in before timing
+
+    def _marshal(self, out, cap):
+        hb = self.hb
+        return self.lib.oracle_marshal_batch(
+            _p(hb.meta), _p(hb.var), len(hb.var), _p(hb.acl), len(hb.acl), _p(hb.regions),
+            len(hb.regions), _p(hb.payload), _p(hb.payload_off), self.n, _p(out), cap,
+            _p(self.out_off), _p(self.status))
+
+    def cycle(self) -> int:
+        self._marshal(self.out, self.total)
+        self.lib.oracle_decode_batch(_p(self.out), _p(self.out_off), self.n, _p(self.meta),
+                                     _p(self.info), _p(self.acl), len(self.acl), _p(self.reg),
+                                     len(self.reg), _p(self.data), len(self.data), _p(self.totals))
+        return self.total
+
+
 def key(row, meta_status: int):
     out = (C.c_uint8 * 29)()
     row = np.ascontiguousarray(row)

@@ -117,3 +117,35 @@ def test_static_and_ticket_launches_alternate(oracle_lib):
         dm.check(oracle_lib, *mid[:2])
     finally:
         c.close()
+
+
+def test_static_tiles_beside_a_copy_that_fills_the_chip(oracle_lib):
+    """Static tiles rely on in-order workgroup dispatch (lookback.h): with a
+    long copy on another stream holding the CUs, the decode's grid is not
+    resident at once, and a wave may wait on a tile whose workgroup has not
+    started. Dispatch in blockIdx order means that workgroup is dispatched
+    first, so the launch completes; results stay bit-exact. Also
+    honu_ctx_reset between launches."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    tiles = 2 * 4 * ncu - 3  # every tile has a resident wave slot: static tiles
+    c = hobj.Codec(0, 64 * tiles)
+    try:
+        rec, off, _ = oracle_lib.marshal_batch(gen_host_batch(31, "small", 0, 64 * tiles - 11))
+        d = _Dec(c, rec, off)
+        src = torch.empty(3 << 30, dtype=torch.uint8, device="cuda")
+        dst = torch.empty_like(src)
+        side = torch.cuda.Stream(priority=-1)
+        for k in range(4):
+            with torch.cuda.stream(side):
+                dst.copy_(src)
+                dst.copy_(src)
+            assert d() == 0  # on the codec's stream, beside the copies
+            torch.cuda.synchronize()
+            d.check(oracle_lib, rec, off)
+            if k == 1:
+                assert c.lib.honu_ctx_reset(c.ctx, c.stream) == 0
+        del src, dst
+    finally:
+        c.close()

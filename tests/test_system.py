@@ -274,6 +274,8 @@ def test_gpu_marshal_unmarshal_system_api():
         UnmarshalSystem(b"\x01\x00")
     from honu_amd.system import Unmarshal
     assert Unmarshal(obj[2:-1], Collection()) == normalize_collection(c)
+    into = Collection(Name="stale")  # decoded in place, as lani.Unmarshal(raw, &c)
+    assert Unmarshal(obj[2:-1], into) is into and into == normalize_collection(c)
     with pytest.raises(hobj.GoPanic):  # store.go:155: a nil *Collection
         Unmarshal(obj, None)
     with pytest.raises(hobj.ErrUnexpectedEOF):

@@ -35,16 +35,12 @@ def dev(nbytes, d):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=d)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--records", type=int, default=65536)
-    ap.add_argument("--chunk", type=int, default=4096)
-    ap.add_argument("--shape", default="large")
-    ap.add_argument("--reps", type=int, default=3)
-    a = ap.parse_args()
-    d = torch.device("cuda", 0)
-    N, C = a.records, a.chunk
-    meta, var, acl, reg, off = gen_meta(1, a.shape, 0, N)
+def measure(shape="large", records=65536, chunk=4096, reps=3, device=0, first=0):
+    """Host-path encode and decode rates of records [first, first + records)
+    of the seed-1 synthetic batch on cuda:device (one JSON-able dict)."""
+    d = torch.device("cuda", device)
+    N, C = records, chunk
+    meta, var, acl, reg, off = gen_meta(1, shape, first, N)
     off64 = off.astype(np.int64)
     chunks = [(s, min(s + C, N)) for s in range(0, N, C)]
     rng = np.random.default_rng(1)
@@ -53,7 +49,11 @@ def main():
     h_meta.numpy()[: meta.nbytes] = meta.view(np.uint8)
     pay_n = int(off[N])
     h_pay = pinned(pay_n)
-    h_pay.numpy()[:pay_n] = rng.integers(0, 256, pay_n, dtype=np.uint8)
+    # payload bytes do not change the codec's work: a random 1 MiB block, tiled
+    blk = torch.from_numpy(rng.integers(0, 256, 1 << 20, dtype=np.uint8))
+    hv = h_pay[:pay_n]
+    for o in range(0, pay_n, 1 << 20):
+        hv[o:o + (1 << 20)].copy_(blk[: min(1 << 20, pay_n - o)])
     h_poff = []  # per-chunk relative payload offsets, pinned
     for s, e in chunks:
         t = pinned(8 * (e - s + 1))
@@ -74,7 +74,7 @@ def main():
     slots = []
     for _ in range(2):
         slots.append({
-            "codec": Codec(0, C), "meta": dev(352 * C, d), "poff": dev(8 * (C + 1), d),
+            "codec": Codec(device, C), "meta": dev(352 * C, d), "poff": dev(8 * (C + 1), d),
             "pay": dev(cmax, d), "roff": dev(8 * (C + 1), d), "st": dev(4 * C, d),
             "rec": dev(cmax + 2048 * C, d), "dmeta": dev(352 * C, d), "dinfo": dev(32 * C, d),
             "dacl": dev(20 * acl_cap, d), "dreg": dev(4 * reg_cap, d), "data": dev(cmax + 16 * C, d),
@@ -151,7 +151,7 @@ def main():
     run(True)
     run(False)
     te, td = [], []
-    for _ in range(a.reps):
+    for _ in range(reps):
         t0 = time.perf_counter()
         run(True)
         te.append(time.perf_counter() - t0)
@@ -162,14 +162,26 @@ def main():
     rows = h_rows.numpy()[: 352 * N].view(meta.dtype)
     ok = bool(np.array_equal(rows["pid"], meta["pid"]) and np.array_equal(rows["created"], meta["created"]))
     total = int(rec_pos[-1])
-    res = {"records": N, "shape": a.shape, "chunk_records": C, "record_bytes": total,
+    for sl in slots:
+        sl["codec"].close()
+    res = {"records": N, "shape": shape, "chunk_records": C, "record_bytes": total,
            "encode_host_path_gbs": total / min(te) / 1e9,
            "decode_host_path_gbs": total / min(td) / 1e9,
            "encode_s": min(te), "decode_s": min(td), "rows_match": ok,
            "note": "pinned host buffers, 3 streams (H2D / codec / D2H), 2 device slots; "
                    "encode moves payload+rows in and records out, decode moves records in "
                    "and rows+payloads out"}
-    print(json.dumps(res))
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--records", type=int, default=65536)
+    ap.add_argument("--chunk", type=int, default=4096)
+    ap.add_argument("--shape", default="large")
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    print(json.dumps(measure(a.shape, a.records, a.chunk, a.reps)))
 
 
 if __name__ == "__main__":
