@@ -93,6 +93,23 @@ HONU_DEV uint32_t lane_search(uint64_t pre, uint64_t e) {
     }
     return lo;
 }
+// The same over a 32-bit prefix (one ds_bpermute per step).
+HONU_DEV uint32_t lane_search32(uint32_t pre, uint32_t e) {
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1) {
+        const uint32_t mid = lo + step;
+        const uint32_t v = (uint32_t)__shfl((int)pre, (int)(mid & 63));
+        if (mid < 64 && v <= e) lo = mid;
+    }
+    return lo;
+}
+// Wave exclusive scan of v (32-bit); *total = the wave's sum.
+HONU_DEV uint32_t wave_excl32(uint32_t v, uint32_t &total) {
+    const uint32_t inc = wave_inclusive_scan32(v);
+    total = __builtin_amdgcn_readlane(inc, 63);
+    return inc - v;
+}
 HONU_DEV uint64_t shfl_xor64(uint64_t v, int d) {
     return ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), d) << 32) |
            (uint32_t)__shfl_xor((int)(uint32_t)v, d);

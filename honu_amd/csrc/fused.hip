@@ -18,9 +18,6 @@
 namespace honu {
 
 #define OFF(f) ((int)offsetof(honu_meta, f))
-#ifndef FILL_U
-#define FILL_U 4  // ACL entries per lane in flight in the fill
-#endif
 
 // ------------------------------------------------------------------------
 // decode: Object.Metadata() + Data() + Tombstone() + StorageVersion()
@@ -43,22 +40,163 @@ struct DecodeOut {
                               // 2 no look-back wait, 4 static tiles (with 2)
 };
 
+// The ACL lists (every entry present) of a tile staged into the wave's LDS
+// (its windows, free after the walk) for the table fill: round after round,
+// the aligned 16-byte blocks of a run of whole lists, up to STAGE_SLOTS blocks,
+// land by global_load_lds (one per-lane source block per slot, 1 KB per
+// instruction); the entries are then read from LDS. Lists of more than
+// STAGE_SLOTS blocks (over ~900 entries) are not staged.
+#ifndef STAGE_SLOTS_N
+#define STAGE_SLOTS_N 1216
+#endif
+constexpr uint32_t STAGE_SLOTS = STAGE_SLOTS_N;
+static_assert(STAGE_SLOTS % HONU_WAVE == 0, "whole instructions");
+// a wave's LDS: its windows during the walk, the staging after it (two
+// 4-wave workgroups per CU still fit the 160 KB)
+constexpr uint32_t FUSED_WAVE_BYTES =
+    STAGE_SLOTS * 16 + 32 > WIN_WAVE_BYTES ? STAGE_SLOTS * 16 + 32 : WIN_WAVE_BYTES;
+static_assert(2 * HONU_WAVES_PER_BLOCK * FUSED_WAVE_BYTES + 64 <= 160 * 1024, "2 workgroups per CU");
+
+struct AclStage {
+    uint64_t apos;   // this lane's first flag
+    uint32_t nb, B;  // this lane's blocks, exclusive prefix over the wave
+    uint32_t nacl;   // this lane's staged entries (0: not staged)
+    uint32_t nbtot;  // wave-uniform: all blocks
+    uint32_t start, stop, r0, r1;  // wave-uniform: the round's blocks and lanes
+
+    HONU_DEV void init(bool fl, uint64_t apos_, uint64_t nacl_) {
+        apos = apos_;
+        const uint64_t b = fl ? ((apos + 18 * nacl_ + 15) >> 4) - (apos >> 4) : 0;
+        const bool st = b && b <= STAGE_SLOTS;
+        nb = st ? (uint32_t)b : 0;
+        nacl = st ? (uint32_t)nacl_ : 0;
+        B = wave_excl32(nb, nbtot);
+        start = 0;
+        r0 = 0;
+        plan();
+    }
+    HONU_DEV bool staged() const { return nacl != 0; }
+    HONU_DEV bool more() const { return start < nbtot; }
+    // the round: lanes [r0, r1) whose blocks end within start + STAGE_SLOTS
+    // (B + nb is non-decreasing over the lanes)
+    HONU_DEV void plan() {
+        const uint64_t m = __ballot(B + nb <= start + STAGE_SLOTS);
+        r1 = (uint32_t)__builtin_popcountll(m);
+        stop = r1 < HONU_WAVE ? __builtin_amdgcn_readlane(B, r1) : nbtot;
+    }
+    HONU_DEV void advance() {
+        start = stop;
+        r0 = r1;
+        plan();
+    }
+    // slot s of the round <- block start + s of the wave's list blocks. The
+    // 64 slots of instruction k belong to a few lists: the owner of the first
+    // slot by one ballot, then the lists that start inside the window in a
+    // wave-uniform loop over their lanes (readlane, no lane shuffles).
+    HONU_DEV void issue(uint8_t *ws, const uint8_t *__restrict__ rec) const {
+        const uint32_t lane = lane_id();
+#pragma unroll
+        for (uint32_t k = 0; k < STAGE_SLOTS / HONU_WAVE; k++) {
+            const uint32_t w0 = start + HONU_WAVE * k;
+            if (w0 >= stop) break;  // wave-uniform
+            const uint32_t r = (uint32_t)__builtin_popcountll(__ballot(B <= w0)) - 1;
+            uint32_t rb = __builtin_amdgcn_readlane(B, r);
+            uint64_t ra = readlane64(apos, r);
+            uint64_t heads = __ballot(B > w0 && B < w0 + HONU_WAVE);
+            while (heads) {
+                const uint32_t h = (uint32_t)__builtin_ctzll(heads);
+                heads &= heads - 1;
+                const uint32_t hb = __builtin_amdgcn_readlane(B, h);
+                const uint64_t ha = readlane64(apos, h);
+                if (lane >= hb - w0) {
+                    rb = hb;
+                    ra = ha;
+                }
+            }
+            const uint32_t g = w0 + lane;
+            if (g < stop)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(rec + 16 * ((ra >> 4) + (g - rb))),
+                    (__attribute__((address_space(3))) void *)(ws + 1024 * k), 16, 0, 0);
+        }
+    }
+    // the round's entries, from LDS, to the table (records whose ok is false
+    // store nothing: capacity); lane e of a pass takes entry e of the round,
+    // its list found as in issue()
+    HONU_DEV void store(const uint8_t *ws, honu_acl *__restrict__ acl, uint64_t ao, bool ok) const {
+        const uint32_t lane = lane_id();
+        __builtin_amdgcn_s_waitcnt(0);  // the round's blocks have landed
+        wave_sync();
+        const bool in = lane >= r0 && lane < r1;
+        uint32_t etot;
+        const uint32_t epre = wave_excl32(in ? nacl : 0, etot);
+        // per list: LDS offset of its first flag, table offset, capacity verdict
+        const uint32_t lbase = 16 * (B - start) + (uint32_t)(apos & 15);
+        const uint64_t tdst = ok ? ao : ~0ull;
+        for (uint32_t w0 = 0; w0 < etot; w0 += HONU_WAVE) {  // wave-uniform
+            const uint32_t r = (uint32_t)__builtin_popcountll(__ballot(epre <= w0)) - 1;
+            uint32_t rp = __builtin_amdgcn_readlane(epre, r);
+            uint32_t rl = __builtin_amdgcn_readlane(lbase, r);
+            uint64_t rt = readlane64(tdst, r);
+            uint64_t heads = __ballot(epre > w0 && epre < w0 + HONU_WAVE);
+            while (heads) {
+                const uint32_t h = (uint32_t)__builtin_ctzll(heads);
+                heads &= heads - 1;
+                const uint32_t hp = __builtin_amdgcn_readlane(epre, h);
+                const uint32_t hl = __builtin_amdgcn_readlane(lbase, h);
+                const uint64_t ht = readlane64(tdst, h);
+                if (lane >= hp - w0) {
+                    rp = hp;
+                    rl = hl;
+                    rt = ht;
+                }
+            }
+            const uint32_t e = w0 + lane;
+            const uint32_t j = e - rp;
+            // the ClientID's first byte in LDS, Permissions 16 bytes on
+            const uint32_t q = rl + 18 * j + 1;
+            const uint32_t qa = q & ~15u, sft = q & 15u;
+            const u32x4 a = *reinterpret_cast<const u32x4 *>(ws + qa);
+            const u32x4 b = *reinterpret_cast<const u32x4 *>(ws + qa + 16);
+            uint64_t lo, hi;
+            window16(a, b, sft, lo, hi);
+            const uint32_t bw = (sft >> 2) == 0 ? b.x : (sft >> 2) == 1 ? b.y : (sft >> 2) == 2 ? b.z : b.w;
+            const uint32_t pm = (bw >> (8 * (sft & 3))) & 0xFF;
+            if (e < etot && rt != ~0ull) {
+                uint32_t *d = reinterpret_cast<uint32_t *>(acl + rt + j);
+                d[0] = (uint32_t)lo;
+                d[1] = (uint32_t)(lo >> 32);
+                d[2] = (uint32_t)hi;
+                d[3] = (uint32_t)(hi >> 32);
+                d[4] = pm | (1u << 8);
+            }
+        }
+        wave_sync();  // the LDS is the next round's (or the next tile's windows)
+    }
+};
+
 __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
     DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t lb_words) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * WIN_WAVE_BYTES];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * FUSED_WAVE_BYTES];
     __shared__ uint32_t last_flag;
-    uint8_t *ws = smem + (threadIdx.x / HONU_WAVE) * WIN_WAVE_BYTES;
+    uint8_t *ws = smem + (threadIdx.x / HONU_WAVE) * FUSED_WAVE_BYTES;
     const uint32_t lane = lane_id();
     const uint32_t ep = lb_epoch(lb);
     const uint64_t ntiles = (n + HONU_WAVE - 1) / HONU_WAVE;
     const uint64_t waves = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
     // every tile has a resident wave of its own: static tiles (lookback.h)
     const bool stat = ntiles <= waves && !(O.dbg & 4);
-    uint64_t t;
+    // (measured: taking the next ticket and loading its bounds before the
+    // look-back wait, to overlap them with it, doubled the wait: tiles are
+    // then handed out ~40 us before their waves start them, which spreads the
+    // publish times of consecutive tiles)
+    const bool stat_idx = stat || (O.dbg & 4);  // dbg 4: measurement only (with 2), static tiles at any size
     uint64_t k_static = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + threadIdx.x / HONU_WAVE;
+    WSTAMP_START();
     for (;;) {
-        if (stat || (O.dbg & 4)) {  // dbg 4: measurement only (with 2), static tiles at any size
+        uint64_t t;
+        if (stat_idx) {
             t = k_static;
             k_static += waves;
         } else {
@@ -67,8 +205,11 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         if (t >= ntiles) break;
         const uint64_t i0 = t * HONU_WAVE, i = i0 + lane;
         const bool valid = i < n;
+        TileHead H;
+        tile_head_bounds(i0, rec_off, n, H);
+        tile_head_bytes(rec, H);
         WinParse P;
-        win_walk(i0, ws, rec, rec_off, n, P);
+        win_walk(i0, ws, rec, n, H, P);
 
         // counts -> offsets: wave scan + look-back across tiles
         const uint64_t c0 = P.nacl, c1 = P.nreg, c2 = (P.data_len + 15) & ~15ull;
@@ -77,14 +218,23 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         const uint64_t x1 = wave_excl(c1, agg[1]);
         const uint64_t x2 = wave_excl(c2, agg[2]);
         // publish, then write the rows while the predecessors finish (their
-        // list offsets are patched in below), then wait
+        // list offsets are patched in below)
         if (!(O.dbg & 2)) lb_publish<3>(lb_status, t, ep, agg);
         rows_out(ws, P.R, i0, n, O.meta);
+        // the ACL lists with every entry present go to the table from LDS: the
+        // first round of their blocks is staged now, before the wait, as it
+        // needs no offsets
+        const bool fl = valid && P.st == HONU_OK && P.nacl && (P.acl_pos & GRP_ACL_FAST);
+        AclStage S;
+        S.init(fl, P.acl_pos & GRP_POS_MASK, P.nacl);
+        if (S.more() && !(O.dbg & 1)) S.issue(ws, rec);
+        WSTAMP(10);  // publish + rows out + first staging round issued
         if (O.dbg & 2) {
             excl[0] = excl[1] = excl[2] = 0;
         } else {
             lb_resolve<3>(lb_status, t, ep, agg, excl);
         }
+        WSTAMP(11);  // look-back wait
         if (t == ntiles - 1 && lane < 3)
             O.totals[lane] = lane == 0 ? excl[0] + agg[0] : (lane == 1 ? excl[1] + agg[1] : excl[2] + agg[2]);
         const uint64_t ao = excl[0] + x0, ro = excl[1] + x1, doff = excl[2] + x2;
@@ -132,13 +282,10 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
                 }
             }
         }
-        // ACL table. Lists with every entry present: the wave's entries are one
-        // run of the table; lane e of a round takes entry e of that run (record
-        // by a search over the lanes' prefixes), reads the 17 bytes after its
-        // flag (the walk fetched them moments ago) and stores the 20-byte row.
-        const bool fast = ok && P.nacl && (P.acl_pos & GRP_ACL_FAST);
+        // ACL table, lists the staging does not take (nil entries, or longer
+        // than one round): the lane walks its list from global memory
         const uint64_t apos = P.acl_pos & GRP_POS_MASK;
-        if (ok && P.nacl && !fast) {  // nil entries: the lane walks its list (validated)
+        if (ok && P.nacl && !S.staged()) {
             uint64_t p = apos;
             for (uint64_t k = 0; k < P.nacl; k++) {
                 uint32_t *d = reinterpret_cast<uint32_t *>(O.acl + ao + k);
@@ -157,46 +304,34 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
                 }
             }
         }
-        uint64_t ftot;
-        const uint64_t fpre = wave_excl(fast ? P.nacl : 0, ftot);
-        constexpr int U = FILL_U;  // entries per lane in flight
+        WSTAMP(12);  // info, regions, lists with nil entries
+        // staged lists: round by round, lane e of a pass takes entry e of the
+        // round's entries (one run of the table per record), reads its 17
+        // bytes from LDS and stores the 20-byte row
         if (!(O.dbg & 1))
-        for (uint64_t e0 = 0; e0 < ftot; e0 += U * HONU_WAVE) {  // wave-uniform
-            u32x4 id[U];
-            uint32_t pm[U];
-            uint64_t dst[U];
-#pragma unroll
-            for (int k = 0; k < U; k++) {
-                const uint64_t e = e0 + lane + HONU_WAVE * k;
-                const uint32_t r = lane_search(fpre, e < ftot ? e : 0);
-                const uint64_t rp = shfl64(fpre, r), ra = shfl64(apos, r), rao = shfl64(ao, r);
-                const uint64_t j = e - rp;
-                const uint64_t q = ra + 18 * j + 1;  // ClientID, then Permissions at q + 16
-                dst[k] = rao + j;
-                if (e < ftot) {  // one unaligned 16-byte load + one byte
-                    id[k] = *reinterpret_cast<const u32x4u *>(rec + q);
-                    pm[k] = rec[q + 16];
-                }
+            while (S.more()) {
+                S.store(ws, O.acl, ao, ok);
+                S.advance();
+                if (S.more()) S.issue(ws, rec);
             }
-#pragma unroll
-            for (int k = 0; k < U; k++) {
-                const uint64_t e = e0 + lane + HONU_WAVE * k;
-                if (e < ftot) {
-                    uint32_t *d = reinterpret_cast<uint32_t *>(O.acl + dst[k]);
-                    d[0] = id[k].x;
-                    d[1] = id[k].y;
-                    d[2] = id[k].z;
-                    d[3] = id[k].w;
-                    d[4] = pm[k] | (1u << 8);
-                }
-            }
-        }
+        WSTAMP(13);  // ACL fill
     }
-    if (stat)
-        lb_finish_blocks(lb, lb_status, lb_words, gridDim.x, &last_flag);
-    else if (!(O.dbg & 4))
-        lb_finish(lb, lb_status, lb_words, t, ntiles, (uint32_t)waves);
+    lb_finish_blocks(lb, lb_status, lb_words, gridDim.x, &last_flag);
 }
+
+#ifdef HONU_STAGE_TIMING
+extern "C" int32_t honu_debug_stage_times(void *host, uint64_t waves, int32_t reset) {
+    if (reset) {
+        static uint64_t zero[1 << 16][STAGES_MAX];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_stage), zero, sizeof zero) != hipSuccess) return -1;
+        return 0;
+    }
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stage), waves * STAGES_MAX * sizeof(uint64_t)) ==
+                   hipSuccess
+               ? 0
+               : -1;
+}
+#endif
 
 hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                honu_meta *meta, honu_record_info *info, honu_acl *acl,

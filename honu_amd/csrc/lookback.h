@@ -158,9 +158,12 @@ HONU_DEV void lb_finish(LbState *s, uint64_t *status, uint64_t status_words, uin
 // this grid is not resident all at once (tests/test_lookback.py runs the
 // decode in this mode beside a copy that fills the CUs). Saves the launch-time burst of ticket
 // atomics on one address (~20 us for 2048 waves). The last workgroup to
-// finish (one atomic per workgroup) resets the count and advances the epoch;
-// on a wrap of the epoch it clears the status array first. Called by every
-// thread of the workgroup; flag: one word of LDS.
+// finish (one atomic per workgroup) resets the count and the ticket and
+// advances the epoch; on a wrap of the epoch it clears the status array first.
+// Also the end of a ticket launch whose waves take their next ticket before
+// finishing the current tile (the ticket order alone then no longer tells
+// which wave ends last). Called by every thread of the workgroup; flag: one
+// word of LDS.
 HONU_DEV void lb_finish_blocks(LbState *s, uint64_t *status, uint64_t status_words, uint32_t nblocks,
                                uint32_t *flag) {
     __syncthreads();
@@ -175,6 +178,7 @@ HONU_DEV void lb_finish_blocks(LbState *s, uint64_t *status, uint64_t status_wor
     __syncthreads();
     if (threadIdx.x == 0) {
         __hip_atomic_store(&s->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&s->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&s->epoch, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
 }

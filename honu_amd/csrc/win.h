@@ -189,9 +189,37 @@ static __device__ uint64_t g_walk_stamps[1 << 16][WALK_STAMPS];  // per translat
         const uint64_t wid_ = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + threadIdx.x / 64; \
         if (lane_id() == 0 && wid_ < (1 << 16)) g_walk_stamps[wid_][k] = wall_clock64();      \
     } while (0)
+#elif defined(HONU_STAGE_TIMING)
+// Timing build only (-DHONU_STAGE_TIMING, tools/fused_timing.py): lane 0 of
+// every wave ADDS the time since its previous stamp to stage k, over every tile
+// the wave takes, so the sums divided by the tiles give the stage costs under
+// full load (the single-launch decode stamps its post-walk stages as 10..13).
+#define STAGES_MAX 16
+static __device__ uint64_t g_stage[1 << 16][STAGES_MAX];
+static __device__ uint64_t g_stage_last[1 << 16];
+#define STAGE_WID() ((uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + threadIdx.x / 64)
+#define WSTAMP(k)                                                          \
+    do {                                                                   \
+        const uint64_t wid_ = STAGE_WID();                                 \
+        if (lane_id() == 0 && wid_ < (1 << 16)) {                          \
+            const uint64_t now_ = wall_clock64();                          \
+            g_stage[wid_][k] += now_ - g_stage_last[wid_];                 \
+            g_stage_last[wid_] = now_;                                     \
+        }                                                                  \
+    } while (0)
+#define WSTAMP_START()                                                     \
+    do {                                                                   \
+        const uint64_t wid_ = STAGE_WID();                                 \
+        if (lane_id() == 0 && wid_ < (1 << 16)) g_stage_last[wid_] = wall_clock64(); \
+    } while (0)
 #else
 #define WSTAMP(k) \
     do {          \
+    } while (0)
+#endif
+#ifndef WSTAMP_START
+#define WSTAMP_START() \
+    do {               \
     } while (0)
 #endif
 
@@ -210,12 +238,40 @@ struct WinParse {
     uint32_t tomb;
 };
 
+// The first bytes of a tile's records: the record bounds and the 16 bytes at
+// each record's start (header). Loaded apart from the walk so that a wave can
+// issue the next tile's loads while it finishes the current one.
+struct TileHead {
+    uint64_t beg, end;
+    u32x4 a, b;  // the aligned blocks holding [beg, beg + 16) (b only when needed)
+};
+// rec_off[i], rec_off[i + 1] of record i0 + lane (0, 0 past n)
+HONU_DEV void tile_head_bounds(uint64_t i0, const uint64_t *__restrict__ rec_off, uint64_t n,
+                               TileHead &H) {
+    const uint64_t i = i0 + lane_id();
+    H.beg = H.end = 0;
+    if (i < n) {
+        H.beg = rec_off[i];
+        H.end = rec_off[i + 1];
+    }
+}
+// the header blocks (lane_fetch16 without the funnel)
+HONU_DEV void tile_head_bytes(const uint8_t *__restrict__ rec, TileHead &H) {
+    H.a = u32x4{0, 0, 0, 0};
+    H.b = u32x4{0, 0, 0, 0};
+    if (H.end > H.beg) {
+        const uint64_t A = H.beg & ~15ull;
+        H.a = *reinterpret_cast<const u32x4 *>(rec + A);
+        if ((H.beg & 15) && A + 16 < H.end) H.b = *reinterpret_cast<const u32x4 *>(rec + A + 16);
+    }
+}
+
 // Object.Metadata() + Data() + Tombstone() + StorageVersion() (object.go:47-134)
 // of record i0 + lane, the lani walk of metadata.go:202-302. Wave-uniform
 // call (every lane of the wave, i0 the same): the window refills need the
-// whole wave.
+// whole wave. H: the tile's bounds and header bytes (tile_head_*).
 HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restrict__ rec,
-                       const uint64_t *__restrict__ rec_off, uint64_t n, WinParse &P) {
+                       uint64_t n, const TileHead &H, WinParse &P) {
 #define OFF(f) ((int)offsetof(honu_meta, f))
 #define STEP(x)                      \
     do {                             \
@@ -225,11 +281,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
     const uint64_t i = i0 + lane;
     const bool valid = i < n;
     WSTAMP(0);  // walk entered
-    uint64_t beg = 0, end = 0;
-    if (valid) {
-        beg = rec_off[i];
-        end = rec_off[i + 1];
-    }
+    const uint64_t beg = H.beg, end = H.end;
     LaneWin W;
     WSTAMP(1);  // rec_off loaded
     W.init(wave_smem, rec, end);
@@ -238,7 +290,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
     int64_t d = -1, b = -1;
     if (valid && len) {
         uint64_t lo, hi;
-        lane_fetch16(rec, beg, end, lo, hi);
+        window16(H.a, H.b, (uint32_t)(beg & 15), lo, hi);
         ver = (uint32_t)(lo & 0xFF);
         // dataLength (object.go:114-134): Uvarint(o[1 : min(11, len-1)])
         if (len >= 3) {

@@ -28,7 +28,10 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_win(
     for (uint64_t i0 = (uint64_t)blockIdx.x * HONU_BLOCK + wv * HONU_WAVE; i0 < n;
          i0 += (uint64_t)gridDim.x * HONU_BLOCK) {
         WinParse P;
-        win_walk(i0, ws, rec, rec_off, n, P);
+        TileHead H;
+        tile_head_bounds(i0, rec_off, n, H);
+        tile_head_bytes(rec, H);
+        win_walk(i0, ws, rec, n, H, P);
         rows_out(ws, P.R, i0, n, meta);
         const uint64_t i = i0 + lane_id();
         if (i >= n) continue;
