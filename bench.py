@@ -74,7 +74,7 @@ def parse_args(argv=None):
     p.add_argument("--lane-blocks", type=int, default=-1,
                    help="workgroups per CU for the lane/group metadata kernels while copies run "
                         "beside them (0 = no cap; -1 = auto: 2 when records average > 64 KiB, "
-                        "where the copies dominate, 4 above 8 KiB, else no cap)")
+                        "where the copies dominate, else no cap)")
     p.add_argument("--copy-prio", type=int, default=1, help="copy stream gets high priority")
     p.add_argument("--encode-copy-after", choices=["scan", "meta"], default="scan",
                    help="start a chunk's encode payload copy after its sizes + scan, or after "
@@ -91,6 +91,9 @@ def parse_args(argv=None):
     p.add_argument("--decode-leg", choices=["both", "zero_copy", "materialising"], default="both",
                    help="decode mode: run one leg only (PMC passes attribute a kernel's traffic "
                         "to one leg)")
+    p.add_argument("--no-host-path", action="store_true",
+                   help="encdec mode: skip the host-path leg (PMC passes: its small launches "
+                        "would mix into the copy kernels' per-launch averages)")
     p.add_argument("--no-decode-legs", action="store_true",
                    help="encdec mode: skip the whole-batch decode legs run after the timed steps")
     return p.parse_args(argv)
@@ -187,9 +190,11 @@ class Bench:
                       for _ in range(nslots)]
         ncu = torch.cuda.get_device_properties(self.dev).multi_processor_count
         lane_blocks = args.lane_blocks
-        if lane_blocks < 0:  # measured: tools/overlap_sweep.sh, tools/ab_env.sh
+        if lane_blocks < 0:  # measured: tools/overlap_sweep.sh, tools/ab_env.sh, tools/args_ab.sh
             avg = self.total_rec_bytes / N
-            lane_blocks = 2 if avg > 65536 else (4 if avg > 8192 else 0)
+            # round 3: no cap below 64 KiB (1M Medium 1048-1050 uncapped vs 1032-1034
+            # GiB/s capped at 4 per CU, profiles/r03/medium_lane_blocks_ab.txt)
+            lane_blocks = 2 if avg > 65536 else 0
         self.lane_blocks = 0 if args.serial else lane_blocks
         for sl in self.slots:
             if args.copy_blocks:
@@ -238,6 +243,9 @@ class Bench:
         for a, b in self.chunks:
             sl = self._issue(a, b, timed)
             if check is not None:
+                if len(self.slots) == 1:  # --serial: the next chunk reuses the one slot
+                    ok &= self._check(check, (a, b, sl))
+                    continue
                 if pending is not None:
                     ok &= self._check(check, pending)
                 pending = (a, b, sl)
@@ -1171,7 +1179,8 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
         scatter = scatter_leg(arena, off, dist, world, all_ok, gpu_parse_check(local),
                               torch.cuda.synchronize)
     bench.release()
-    host_path = host_path_leg(bench, args, local, world, gather_max, all_ok)
+    host_path = None if args.no_host_path else host_path_leg(bench, args, local, world, gather_max,
+                                                             all_ok)
     decode = None if args.no_decode_legs else decode_legs(bench, args, world, barrier, gather_max,
                                                           all_ok)
     if rank != 0:

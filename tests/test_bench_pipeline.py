@@ -141,3 +141,14 @@ def test_encode_payloads_respects_out_cap(oracle_lib):
         hl = 1 + len(oracle_lib.put_uvarint(plen))
         assert h[s + hl:s + hl + plen].tobytes() == oout[s + hl:s + hl + plen].tobytes()
     codec.close()
+
+
+def test_bench_serial_verify(oracle_lib):
+    """--serial (one stream, one output slot): each chunk is checked before
+    the next one reuses the slot, and the bench's own verification passes."""
+    args = bench.parse_args(["--records", "3000", "--shape", "small", "--min-chunks", "3",
+                             "--serial"])
+    b = bench.Bench(args, 0, 0)
+    assert len(b.slots) == 1 and len(b.chunks) == 3
+    b.step()
+    assert b.verify()
