@@ -1030,7 +1030,7 @@ def host_path_leg(bench, args, local, world, gather_max, all_ok, measure=None):
         from tools.host_path import measure
     avg = bench.total_rec_bytes / bench.N
     n = int(max(256, min(bench.N, (4 << 30) // max(1, int(avg)))))
-    chunk = int(max(256, n // 8))  # ~512 MiB per transfer (PCIe-rate chunks)
+    chunk = int(max(256, n // 16))  # 16 transfers: the pipeline fill and drain are 2 of them
     r = measure(args.shape, n, chunk, reps=2, device=local, first=bench.first)
     enc_s, _ = gather_max(r["encode_s"])
     dec_s, _ = gather_max(r["decode_s"])
