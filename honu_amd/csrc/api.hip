@@ -137,6 +137,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->geom.copy_blocks = env_int("HONU_COPY_BLOCKS", prop.multiProcessorCount * 2);
     c->geom.copy_variant = HONU_AB_BUILD ? env_int("HONU_COPY_VARIANT", 0) : 0;
     c->geom.record_variant = env_int("HONU_RECORD_VARIANT", 0);
+    c->geom.encode_variant = env_int("HONU_ENCODE_VARIANT", 0) == 1 ? 1 : 0;  // 0 default
     if (c->geom.record_variant != 5 && c->geom.record_variant != 6)
         c->geom.record_variant = 0;
     const uint64_t n = c->max_n;
@@ -214,6 +215,8 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
     else if (!strcmp(name, "lane_blocks") && value >= 0) ctx->geom.lane_blocks = (int)value;
     else if (!strcmp(name, "copy_variant") && value >= 0 && (value == 0 || HONU_AB_BUILD))
         ctx->geom.copy_variant = (int)value;
+    else if (!strcmp(name, "encode_variant") && (value == 0 || value == 1))
+        ctx->geom.encode_variant = (int)value;
     else if (!strcmp(name, "record_variant") &&
              (value == 0 || value == 5 || value == 6))
         ctx->geom.record_variant = (int)value;
@@ -257,9 +260,16 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
         return arg_fail("null pointer");
     if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
     HIPCHK(hipSetDevice(ctx->device));
-    // header + tail with the ACL lists' partial end chunks (one record per
-    // lane), then the lists' whole chunks (16 lanes per record)
     if (n > ctx->max_n) return HONU_E_WORKSPACE;
+    if (ctx->geom.encode_variant == 1) {  // one launch, 16 lanes per record (enc.hip)
+        HIPCHK(launch_encode_tail_grp(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
+                                      out_cap, d_out_off, d_status, ctx->geom.lane_blocks,
+                                      (hipStream_t)stream));
+        return HONU_OK;
+    }
+    // encode_variant 0 (default, measured faster: DESIGN §3): header + tail
+    // with the ACL lists' partial end chunks (one record per lane), then the
+    // lists' whole chunks (16 lanes per record)
     HIPCHK(launch_encode_meta_lane(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
                                    out_cap, d_out_off, d_status, ctx->enc_acl,
                                    ctx->geom.lane_blocks, (hipStream_t)stream));

@@ -84,6 +84,8 @@ struct LaunchGeom {
                             // (0: one block per 256 lanes of work, no cap)
     int copy_blocks;        // blocks of the byte-balanced copy kernel
     int copy_variant;       // copy engine variant (copy.hip: unroll depth / cache policy)
+    int encode_variant;     // header/tail encoder: 0 lane writer + ACL group kernel
+                            // (lane.hip, grp.hip; default), 1 group layout (enc.hip)
     int record_variant;     // per-record kernels: 0 auto (the fastest measured form
                             // of each; honu_decode_batch single-launch from 48 K
                             // records), 5 split decode, 6 single-launch decode
@@ -115,6 +117,12 @@ hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, co
 hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uint64_t n,
                                  uint8_t *out, const int32_t *status, const uint64_t *acl_pos,
                                  int max_blocks, hipStream_t s);
+// header + Metadata tail, ACL entries included, one record per 16-lane group
+// (enc.hip; encode_variant 1)
+hipError_t launch_encode_tail_grp(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
+                                  const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
+                                  uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
+                                  int32_t *status, int max_blocks, hipStream_t s);
 
 hipError_t launch_encode_sizes_grp(const honu_meta *meta, uint64_t var_len, const honu_acl *acl,
                                    uint64_t acl_len, const uint32_t *reg, uint64_t reg_len,

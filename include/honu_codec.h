@@ -205,9 +205,13 @@ int32_t honu_ctx_reset(honu_ctx *ctx, void *stream);
  * per-record metadata kernels map records to lanes: 0 auto — the fastest
  * measured form per kernel, with honu_decode_batch running the single-launch
  * decode for batches of 48 K records or more; 5 the split decode at every
- * size; 6 the single-launch decode at every size). Also
+ * size; 6 the single-launch decode at every size), "encode_variant" (the
+ * header/tail encoder of honu_encode_records: 0 one record per lane + the ACL
+ * lists by 16-lane groups, the default; 1 one record per 16-lane group laid
+ * out by a prefix sum over the grammar's slots, same bytes). Also
  * settable at context creation through the environment (HONU_COPY_BLOCKS,
- * HONU_RECORD_BLOCKS, HONU_LANE_BLOCKS, HONU_COPY_VARIANT, HONU_RECORD_VARIANT). */
+ * HONU_RECORD_BLOCKS, HONU_LANE_BLOCKS, HONU_COPY_VARIANT, HONU_RECORD_VARIANT,
+ * HONU_ENCODE_VARIANT). */
 int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value);
 
 /* ABI self-description, used by bindings to check struct layouts. */

@@ -21,17 +21,20 @@ from honu_amd.metadata import META_DTYPE, normalize, pack_batch, unpack_row  # n
 from honu_amd.workload import gen_host_batch, gen_meta  # noqa: E402
 
 
-@pytest.fixture(scope="module", params=[6, 5], ids=["fused", "split"])
+@pytest.fixture(scope="module", params=[(6, 0), (5, 1)], ids=["fused", "split"])
 def codec(request):
-    """Both metadata decodes of the product library: the single-launch decode
-    (fused.hip) at every batch size, and the split kernels (group size pass,
-    lane encode with group ACL lists, windowed lane parse, group fill). The
-    default picks one by batch size; the bench pipeline and large-batch tests
-    run it."""
+    """Both metadata decodes and both header/tail encoders of the product
+    library: the single-launch decode (fused.hip) at every batch size with the
+    default lane encoder + group ACL lists (lane.hip, grp.hip), and the split
+    decode kernels (windowed lane parse, group fill) with the group-layout
+    encoder (enc.hip, encode_variant 1). The default picks the decode by batch
+    size; the bench pipeline and large-batch tests run it."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     c = hobj.Codec(0, 1 << 18)
-    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", request.param), "param")
+    rv, ev = request.param
+    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", rv), "param")
+    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"encode_variant", ev), "param")
     yield c
     c.close()
 

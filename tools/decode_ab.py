@@ -60,6 +60,10 @@ def child(a):
         scrub = E(1 << 30) if a.cold else None
 
         def once():
+            if a.what == "encode":  # header/tail encoder (honu_encode_records), payload copy apart
+                _lib.check(L.honu_encode_records(c, P(dm), P(dv), P(da), P(dr), P(do), n, P(rec),
+                                                 total, P(oo), P(st), s), "encode_records")
+                return
             _lib.check(L.honu_decode_batch(c, P(rec), P(oo), n, P(dmeta), P(dinfo), P(dacl), acl_cap,
                                            P(dreg), reg_cap, 0, 0, P(tot), s), "decode")
         once()
@@ -74,7 +78,7 @@ def child(a):
             torch.cuda.synchronize()
             ms.append(e0.elapsed_time(e1))
         ms.sort()
-        out_lines.append({"workload": wl, "ms_median": ms[len(ms) // 2], "ms_min": ms[0],
+        out_lines.append({"what": a.what, "workload": wl, "ms_median": ms[len(ms) // 2], "ms_min": ms[0],
                           "records_per_s": n / (ms[len(ms) // 2] / 1e3)})
         codec.close()
         del rec, dmeta, dinfo, dacl, dreg, scrub
@@ -89,6 +93,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--reps", type=int, default=9)
     ap.add_argument("--cold", action="store_true", help="1 GiB write before every launch")
+    ap.add_argument("--what", choices=["decode", "encode"], default="decode")
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
     if a.child:
@@ -99,7 +104,7 @@ def main():
         for lib in libs:
             env = dict(os.environ, HONU_LIB_PATH=os.path.abspath(lib))
             cmd = [sys.executable, os.path.abspath(__file__), "--child", "--workloads", a.workloads,
-                   "--reps", str(a.reps)] + (["--cold"] if a.cold else [])
+                   "--reps", str(a.reps), "--what", a.what] + (["--cold"] if a.cold else [])
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
             if p.returncode:
                 print(json.dumps({"round": r, "lib": lib, "error": p.stderr[-2000:]}), flush=True)
