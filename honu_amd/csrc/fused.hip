@@ -46,6 +46,18 @@ struct DecodeOut {
 // land by global_load_lds (one per-lane source block per slot, 1 KB per
 // instruction); the entries are then read from LDS. Lists of more than
 // STAGE_SLOTS blocks (over ~900 entries) are not staged.
+// FUSED_MEMROW 1: rows stored field by field during the walk (win.h MemRow)
+// instead of held in registers and written out through LDS afterwards. It
+// frees 81 VGPRs (244 -> 163, enough for 3 waves per SIMD) but measured 30 %
+// slower at the same occupancy (1M Small 0.856 -> 1.115 ms, a Large chunk
+// +3 %, profiles/r03/fused_memrow_ab.jsonl): vmcnt counts stores on gfx950,
+// so every window refill's wait also waits for the scattered row stores
+// issued before it (the walk's LDS-only stages doubled: fields to the ACL
+// count 7.3 -> 15.6 us per tile). Kept for measurement; the default holds
+// the row in registers.
+#ifndef FUSED_MEMROW
+#define FUSED_MEMROW 0
+#endif
 #ifndef STAGE_SLOTS_N
 #define STAGE_SLOTS_N 1216
 #endif
@@ -209,7 +221,13 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         tile_head_bounds(i0, rec_off, n, H);
         tile_head_bytes(rec, H);
         WinParse P;
-        win_walk(i0, ws, rec, n, H, P);
+#if FUSED_MEMROW
+        MemRow R;
+        R.p = valid ? reinterpret_cast<uint8_t *>(O.meta + i) : nullptr;
+#else
+        RegRow R;
+#endif
+        win_walk(i0, ws, rec, n, H, R, P);
 
         // counts -> offsets: wave scan + look-back across tiles
         const uint64_t c0 = P.nacl, c1 = P.nreg, c2 = (P.data_len + 15) & ~15ull;
@@ -220,7 +238,9 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         // publish, then write the rows while the predecessors finish (their
         // list offsets are patched in below)
         if (!(O.dbg & 2)) lb_publish<3>(lb_status, t, ep, agg);
-        rows_out(ws, P.R, i0, n, O.meta);
+#if !FUSED_MEMROW
+        rows_out(ws, R, i0, n, O.meta);
+#endif
         // the ACL lists with every entry present go to the table from LDS: the
         // first round of their blocks is staged now, before the wait, as it
         // needs no offsets

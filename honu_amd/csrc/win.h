@@ -223,9 +223,78 @@ static __device__ uint64_t g_stage_last[1 << 16];
     } while (0)
 #endif
 
+// Where the walk puts the decoded row (metadata.go:202-302 field by field).
+// RegRow: the whole 352-byte row in 88 registers, out in one coalesced pass
+// afterwards (rows_out). MemRow: every field stored to the lane's row as it is
+// decoded, the fields of absent sub-structs zeroed when their nil flag is
+// read, the whole row zeroed when the walk fails (Go returns nil, err) or the
+// Metadata is nil (object.go:76-82) — 88 registers fewer, scattered stores.
+struct RegRow : Row {
+    HONU_DEV void begin() { clear(); }
+    template <int OFF, int LEN> HONU_DEV void zero() {}  // begin() cleared it
+    HONU_DEV void finish(bool st_ok, bool hm, uint32_t pr) {
+        (void)hm;
+        u32((int)offsetof(honu_meta, present), pr);
+        if (!st_ok) clear();
+    }
+};
+struct MemRow {
+    uint8_t *p;      // this lane's row, nullptr past n
+    uint32_t b0, b1;  // row bytes 4..11 (permissions .. signature_alg, pad)
+
+    HONU_DEV void begin() { b0 = b1 = 0; }
+    HONU_DEV void s32(int off, uint32_t v) {
+        if (p) *reinterpret_cast<uint32_t *>(p + off) = v;
+    }
+    HONU_DEV void s64(int off, uint64_t v) {
+        if (p) *reinterpret_cast<uint64_t *>(p + off) = v;
+    }
+    HONU_DEV void s128(int off, uint64_t lo, uint64_t hi) {
+        if (p)
+            *reinterpret_cast<u32x4 *>(p + off) =
+                u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+    }
+    HONU_DEV void u8(int off, uint32_t v) {  // bytes 4..10, stored by finish()
+        if (off < 8) b0 |= (v & 0xFF) << (8 * (off - 4));
+        else b1 |= (v & 0xFF) << (8 * (off - 8));
+    }
+    HONU_DEV void u32(int off, uint32_t v) { s32(off, v); }
+    HONU_DEV void u64(int off, uint64_t v) { s64(off, v); }
+    HONU_DEV void bytes16(int off, uint64_t lo, uint64_t hi) { s128(off, lo, hi); }
+    HONU_DEV void span(int off, uint64_t o, uint64_t l) { s128(off, o, l); }
+    // zeros over [OFF, OFF + LEN) (compile-time, 4-aligned), widest stores first
+    template <int OFF, int LEN> HONU_DEV void zero() {
+        static_assert(OFF % 4 == 0 && LEN % 4 == 0, "dword granularity");
+        if constexpr (LEN > 0) {
+            if constexpr (OFF % 16 == 0 && LEN >= 16) {
+                s128(OFF, 0, 0);
+                zero<OFF + 16, LEN - 16>();
+            } else if constexpr (OFF % 8 == 0 && LEN >= 8) {
+                s64(OFF, 0);
+                zero<OFF + 8, LEN - 8>();
+            } else {
+                s32(OFF, 0);
+                zero<OFF + 4, LEN - 4>();
+            }
+        }
+    }
+    HONU_DEV void finish(bool st_ok, bool hm, uint32_t pr) {
+        if (!(st_ok && hm)) {  // every byte zero (present too)
+            zero<0, (int)sizeof(honu_meta)>();
+            return;
+        }
+        s32(0, pr);
+        s32(4, b0);
+        s32(8, b1);
+        s32(60, 0);                                   // padding
+        s64(88, 0);
+        s64((int)offsetof(honu_meta, acl_off), 0);    // set after the offsets scan
+        s64((int)offsetof(honu_meta, regions_off), 0);
+    }
+};
+
 // What the walk of one record leaves in the lane's registers.
 struct WinParse {
-    Row R;              // the decoded row (acl_off / regions_off not yet set)
     int st;             // Metadata() status; HONU_SKIP for a lane past n
     uint64_t nacl, nreg;
     uint64_t acl_pos;   // first ACL entry flag, | GRP_ACL_FAST when every entry is present
@@ -269,9 +338,11 @@ HONU_DEV void tile_head_bytes(const uint8_t *__restrict__ rec, TileHead &H) {
 // Object.Metadata() + Data() + Tombstone() + StorageVersion() (object.go:47-134)
 // of record i0 + lane, the lani walk of metadata.go:202-302. Wave-uniform
 // call (every lane of the wave, i0 the same): the window refills need the
-// whole wave. H: the tile's bounds and header bytes (tile_head_*).
+// whole wave. H: the tile's bounds and header bytes (tile_head_*). The row
+// goes to R (RegRow / MemRow, acl_off / regions_off not yet set).
+template <class RowT>
 HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restrict__ rec,
-                       uint64_t n, const TileHead &H, WinParse &P) {
+                       uint64_t n, const TileHead &H, RowT &R, WinParse &P) {
 #define OFF(f) ((int)offsetof(honu_meta, f))
 #define STEP(x)                      \
     do {                             \
@@ -321,8 +392,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
     P.tomb = (v1 && d == 0) ? 1 : 0;  // Tombstone :103-112
     P.end = end;
 
-    Row &R = P.R;
-    R.clear();
+    R.begin();
     uint64_t nacl = 0, nreg = 0, acl_pos = 0, reg_pos = 0;
 #pragma unroll
     for (int k = 0; k < REG_INLINE; k++) P.regs[k] = 0;
@@ -361,9 +431,13 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
                 pr |= HONU_HAS_PARENT;
                 STEP(D.u32(u)); R.u32(OFF(parent_pid), u);
                 STEP(D.u64(v)); R.u64(OFF(parent_vid), v);
+            } else {
+                R.template zero<OFF(parent_pid), 12>();
             }
             STEP(D.boolean(f)); R.u8(OFF(tombstone), f);    // :96
             STEP(D.i64(t)); R.u64(OFF(version_created), (uint64_t)t);  // :100
+        } else {
+            R.template zero<OFF(region), 36>();  // region .. version_created
         }
         STEP(D.boolean(f));                                 // :225 Schema
         if (st == HONU_OK && f) {
@@ -372,6 +446,9 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
             STEP(D.u32(u)); R.u32(OFF(schema_major), u);
             STEP(D.u32(u)); R.u32(OFF(schema_minor), u);
             STEP(D.u32(u)); R.u32(OFF(schema_patch), u);
+        } else {
+            R.template zero<OFF(schema_major), 12>();
+            R.template zero<OFF(schema_name), 16>();
         }
         STEP(D.frame(o, l)); R.span(OFF(mime), o, l);       // :231
         STEP(D.ulid(lo, hi)); R.bytes16(OFF(owner), lo, hi);   // :235
@@ -455,8 +532,8 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
                 }
             }
         }
-        R.u64(OFF(acl_count), nacl);
     }
+    if (hm) R.u64(OFF(acl_count), nacl);  // 0 for an empty list (metadata.go:254)
     WSTAMP(5);  // ACL flags checked
     W.refill(hm && st == HONU_OK ? (D.p & ~15ull) : NOWIN);
     WSTAMP(6);  // window after the list
@@ -482,6 +559,9 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
             STEP(D.ulid(lo, hi)); R.bytes16(OFF(client_id), lo, hi);
             STEP(D.frame(o, l)); R.span(OFF(ip_address), o, l);
             STEP(D.frame(o, l)); R.span(OFF(user_agent), o, l);
+        } else {
+            R.template zero<OFF(publisher_id), 32>();
+            R.template zero<OFF(ip_address), 32>();
         }
         STEP(D.boolean(f));                                 // :277 Encryption
         if (st == HONU_OK && f) {
@@ -491,6 +571,8 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
             STEP(D.frame(o, l)); R.span(OFF(encryption_key), o, l);
             STEP(D.frame(o, l)); R.span(OFF(hmac_secret), o, l);
             STEP(D.frame(o, l)); R.span(OFF(signature), o, l);
+        } else {
+            R.template zero<OFF(public_key_id), 64>();
         }
     }
     WSTAMP(7);  // regions .. signature
@@ -507,14 +589,15 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
             pr |= HONU_HAS_COMPRESSION;
             STEP(D.u8(u)); R.u8(OFF(compression_alg), u);   // compression.go:55-67
             STEP(D.i64(t)); R.u64(OFF(compression_level), (uint64_t)t);
+        } else {
+            R.template zero<OFF(compression_level), 8>();
         }
         STEP(D.u8(u)); R.u8(OFF(flags), u);                 // :289
         STEP(D.i64(t)); R.u64(OFF(created), (uint64_t)t);   // :293
         STEP(D.i64(t)); R.u64(OFF(modified), (uint64_t)t);  // :297
     }
-    R.u32(OFF(present), pr);
+    R.finish(st == HONU_OK, hm, pr);
     if (st != HONU_OK) {  // Go returns nil, err
-        R.clear();
         nacl = nreg = 0;
     }
     WSTAMP(9);  // walk done

@@ -31,8 +31,9 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_win(
         TileHead H;
         tile_head_bounds(i0, rec_off, n, H);
         tile_head_bytes(rec, H);
-        win_walk(i0, ws, rec, n, H, P);
-        rows_out(ws, P.R, i0, n, meta);
+        RegRow R;
+        win_walk(i0, ws, rec, n, H, R, P);
+        rows_out(ws, R, i0, n, meta);
         const uint64_t i = i0 + lane_id();
         if (i >= n) continue;
         store_info(info + i, make_info(P, P.data_off, P.data_len, P.data_status, P.st));
