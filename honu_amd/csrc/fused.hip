@@ -58,6 +58,9 @@ struct DecodeOut {
 #ifndef FUSED_MEMROW
 #define FUSED_MEMROW 0
 #endif
+#ifndef FUSED_SPEC
+#define FUSED_SPEC 1
+#endif
 #ifndef STAGE_SLOTS_N
 #define STAGE_SLOTS_N 1216
 #endif
@@ -187,9 +190,37 @@ struct AclStage {
     }
 };
 
+// Speculative publish (the walk's early hook): a tile's counts go to the
+// look-back as soon as its regions are read, ~18 us per tile before the walk
+// ends, so successors wait less. A record failing in a later field has its
+// counts changed to 0; its tile then raises LbState.misspec, and the guarded
+// launch that follows every speculative one redoes the whole batch without
+// speculation (it returns at once when the flag is clear).
+struct SpecPub {
+    bool on;
+    uint64_t *status;
+    uint64_t t;
+    uint32_t ep;
+    uint64_t c0, c1;            // this lane's published counts
+    uint64_t x[3], agg[3];      // in-tile exclusive prefixes, tile aggregates
+    HONU_DEV void counts(uint64_t a, uint64_t r, uint64_t d) {
+        if (!on) return;
+        c0 = a;
+        c1 = r;
+        x[0] = wave_excl(a, agg[0]);
+        x[1] = wave_excl(r, agg[1]);
+        x[2] = wave_excl(d, agg[2]);
+        lb_publish<3>(status, t, ep, agg);
+    }
+};
+
 __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
-    DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t lb_words) {
+    DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t lb_words, int mode) {
+    // mode 0: plain; 1: speculative publish; 2: guarded recovery (runs only
+    // when the speculative launch before it raised misspec)
+    if (mode == 2 && __hip_atomic_load(&lb->misspec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        return;  // every wave of the launch returns: the look-back state is untouched
     __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * FUSED_WAVE_BYTES];
     __shared__ uint32_t last_flag;
     uint8_t *ws = smem + (threadIdx.x / HONU_WAVE) * FUSED_WAVE_BYTES;
@@ -227,17 +258,33 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
 #else
         RegRow R;
 #endif
-        win_walk(i0, ws, rec, n, H, R, P);
+        SpecPub early;
+        early.on = mode == 1 && !(O.dbg & 2);
+        early.status = lb_status;
+        early.t = t;
+        early.ep = ep;
+        win_walk(i0, ws, rec, n, H, R, P, early);
 
         // counts -> offsets: wave scan + look-back across tiles
-        const uint64_t c0 = P.nacl, c1 = P.nreg, c2 = (P.data_len + 15) & ~15ull;
-        uint64_t agg[3], excl[3];
-        const uint64_t x0 = wave_excl(c0, agg[0]);
-        const uint64_t x1 = wave_excl(c1, agg[1]);
-        const uint64_t x2 = wave_excl(c2, agg[2]);
-        // publish, then write the rows while the predecessors finish (their
-        // list offsets are patched in below)
-        if (!(O.dbg & 2)) lb_publish<3>(lb_status, t, ep, agg);
+        uint64_t agg[3], excl[3], x0, x1, x2;
+        if (early.on) {  // published during the walk; a changed count: misspeculation
+            x0 = early.x[0];
+            x1 = early.x[1];
+            x2 = early.x[2];
+            agg[0] = early.agg[0];
+            agg[1] = early.agg[1];
+            agg[2] = early.agg[2];
+            if (__ballot(P.nacl != early.c0 || P.nreg != early.c1) && lane == 0)
+                __hip_atomic_store(&lb->misspec, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const uint64_t c0 = P.nacl, c1 = P.nreg, c2 = (P.data_len + 15) & ~15ull;
+            x0 = wave_excl(c0, agg[0]);
+            x1 = wave_excl(c1, agg[1]);
+            x2 = wave_excl(c2, agg[2]);
+            // publish, then write the rows while the predecessors finish
+            // (their list offsets are patched in below)
+            if (!(O.dbg & 2)) lb_publish<3>(lb_status, t, ep, agg);
+        }
 #if !FUSED_MEMROW
         rows_out(ws, R, i0, n, O.meta);
 #endif
@@ -336,7 +383,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
             }
         WSTAMP(13);  // ACL fill
     }
-    lb_finish_blocks(lb, lb_status, lb_words, gridDim.x, &last_flag);
+    lb_finish_blocks(lb, lb_status, lb_words, gridDim.x, &last_flag, mode == 2);
 }
 
 #ifdef HONU_STAGE_TIMING
@@ -369,8 +416,21 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
     const int dbg = 0;
 #endif
     DecodeOut O{meta, info, acl, acl_cap, reg, reg_cap, data_cap, materialize, scratch, offs, totals, dbg};
+    // speculation pays where tiles queue for tickets (more tiles than resident
+    // waves: 1M Small 0.866 -> 0.840 ms); a launch whose tiles all start at
+    // once gains less than the guarded launch costs (a 62 K-record Large chunk
+    // 87.6 -> 91 us, profiles/r03/fused_spec_ab.jsonl)
+    if (!FUSED_SPEC || tiles <= b * HONU_WAVES_PER_BLOCK) {
+        hipLaunchKernelGGL(k_decode_fused, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
+                           O, lb, lb_status, lb_words, 0);
+        return hipGetLastError();
+    }
+    // speculative launch, then the guarded recovery launch (a no-op unless a
+    // record failed after publishing its counts: malformed input only)
     hipLaunchKernelGGL(k_decode_fused, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
-                       O, lb, lb_status, lb_words);
+                       O, lb, lb_status, lb_words, 1);
+    hipLaunchKernelGGL(k_decode_fused, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
+                       O, lb, lb_status, lb_words, 2);
     return hipGetLastError();
 }
 

@@ -25,10 +25,10 @@
 namespace honu {
 
 struct LbState {
-    uint32_t ticket;  // next tile
-    uint32_t done;    // workgroups finished (static tiles, lb_finish_blocks)
+    uint32_t ticket;   // next tile
+    uint32_t done;     // workgroups finished (static tiles, lb_finish_blocks)
     uint32_t epoch;
-    uint32_t _pad;
+    uint32_t misspec;  // speculative decode: a tile published counts that changed (fused.hip)
 };
 
 constexpr uint32_t LB_EPOCH_BITS = 18;
@@ -165,7 +165,7 @@ HONU_DEV void lb_finish(LbState *s, uint64_t *status, uint64_t status_words, uin
 // which wave ends last). Called by every thread of the workgroup; flag: one
 // word of LDS.
 HONU_DEV void lb_finish_blocks(LbState *s, uint64_t *status, uint64_t status_words, uint32_t nblocks,
-                               uint32_t *flag) {
+                               uint32_t *flag, bool clear_misspec = false) {
     __syncthreads();
     if (threadIdx.x == 0)
         *flag = __hip_atomic_fetch_add(&s->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
@@ -179,6 +179,7 @@ HONU_DEV void lb_finish_blocks(LbState *s, uint64_t *status, uint64_t status_wor
     if (threadIdx.x == 0) {
         __hip_atomic_store(&s->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&s->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (clear_misspec) __hip_atomic_store(&s->misspec, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&s->epoch, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
 }

@@ -293,6 +293,13 @@ struct MemRow {
     }
 };
 
+// The walk's early hook (wave-uniform call, every lane): the record's ACL
+// entry and region counts once the regions are read (0 for a record that has
+// failed so far) and its aligned payload bytes. NoEarly: nothing.
+struct NoEarly {
+    HONU_DEV void counts(uint64_t, uint64_t, uint64_t) {}
+};
+
 // What the walk of one record leaves in the lane's registers.
 struct WinParse {
     int st;             // Metadata() status; HONU_SKIP for a lane past n
@@ -340,9 +347,9 @@ HONU_DEV void tile_head_bytes(const uint8_t *__restrict__ rec, TileHead &H) {
 // call (every lane of the wave, i0 the same): the window refills need the
 // whole wave. H: the tile's bounds and header bytes (tile_head_*). The row
 // goes to R (RegRow / MemRow, acl_off / regions_off not yet set).
-template <class RowT>
+template <class RowT, class EarlyT>
 HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restrict__ rec,
-                       uint64_t n, const TileHead &H, RowT &R, WinParse &P) {
+                       uint64_t n, const TileHead &H, RowT &R, WinParse &P, EarlyT &early) {
 #define OFF(f) ((int)offsetof(honu_meta, f))
 #define STEP(x)                      \
     do {                             \
@@ -552,6 +559,13 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
         for (uint64_t k = REG_INLINE; k < nreg && st == HONU_OK; k++) STEP(D.u32(u));
         if (nreg <= REG_INLINE) reg_pos |= GRP_REG_INLINE;
         R.u64(OFF(regions_count), nreg);
+    }
+    // both list counts are known here; a later field can still fail the
+    // record (its counts then become 0): the early hook publishes them
+    // tentatively (fused.hip speculative decode)
+    early.counts(hm && st == HONU_OK ? nacl : 0, hm && st == HONU_OK ? nreg : 0,
+                 (P.data_len + 15) & ~15ull);
+    if (hm) {
         STEP(D.boolean(f));                                 // :271 Publisher
         if (st == HONU_OK && f) {
             pr |= HONU_HAS_PUBLISHER;

@@ -32,7 +32,8 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_win(
         tile_head_bounds(i0, rec_off, n, H);
         tile_head_bytes(rec, H);
         RegRow R;
-        win_walk(i0, ws, rec, n, H, R, P);
+        NoEarly none;
+        win_walk(i0, ws, rec, n, H, R, P, none);
         rows_out(ws, R, i0, n, meta);
         const uint64_t i = i0 + lane_id();
         if (i >= n) continue;

@@ -149,3 +149,39 @@ def test_static_tiles_beside_a_copy_that_fills_the_chip(oracle_lib):
         del src, dst
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("n,bad", [(5000, [1234]), (64 * 300, [5, 64 * 150 + 3, 64 * 299 + 1]),
+                                   (1000, [999])])
+def test_speculative_publish_recovers(oracle_lib, n, bad):
+    """The single-launch decode publishes a tile's counts once its regions
+    are read (fused.hip SpecPub). Records truncated by a few bytes fail in a
+    later field (the Modified time), so their published counts were wrong:
+    the guarded second launch must redo the batch, bit-exact with the oracle,
+    and clear the flag (a clean batch decoded next on the same context is
+    exact too)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rec, off, _ = oracle_lib.marshal_batch(gen_host_batch(41, "small", 0, n))
+    pieces, noff = [], [0]
+    for i in range(n):
+        r = rec[int(off[i]):int(off[i + 1])]
+        if i in bad:
+            r = r[:-3]
+        pieces.append(r)
+        noff.append(noff[-1] + len(r))
+    brec = np.concatenate(pieces)
+    boff = np.array(noff, np.uint64)
+    c = hobj.Codec(0, n)
+    try:
+        hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
+        d = _Dec(c, brec, boff)
+        assert d() == 0
+        d.check(oracle_lib, brec, boff)
+        info = d.info[:32 * n].cpu().numpy().view(np.int32).reshape(n, 8)
+        assert all(info[i, 5] != 0 for i in bad)  # meta_status of the truncated records
+        good = _Dec(c, rec, off)
+        assert good() == 0
+        good.check(oracle_lib, rec, off)
+    finally:
+        c.close()
