@@ -575,12 +575,13 @@ class DecodeBench:
             "calls": "honu_decode_batch(data arena NULL) over all records, one call",
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_decode_fused",
+                "kernel": "k_decode_fused (speculative launch; the guarded one returns at once)",
                 "achieved": gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": gbs / HBM_PEAK_GBS,
-                "traffic": pmc_traffic(self.workload("zero_copy"), "k_decode_fused"),
+                "traffic": (pmc_traffic(self.workload("zero_copy"), "k_decode_fused<1>")
+                            or pmc_traffic(self.workload("zero_copy"), "k_decode_fused<0>")),
                 "avg_launch_ms": t * 1e3,
                 "algorithmic_bytes_per_launch": self.meta_bytes,
                 "algorithmic_bytes": "8 (offsets) + header + Metadata tail read; 352 row + 32 info "
@@ -1025,7 +1026,8 @@ def decode_legs(bench, args, world, barrier, gather_max, all_ok):
 def host_path_leg(bench, args, local, world, gather_max, all_ok, measure=None):
     """SURVEY §8d/§8e host path on every rank at once: pinned H2D -> codec ->
     D2H of a ~4 GiB sample of the rank's own records (tools/host_path.py
-    measure); aggregate = all ranks' bytes / the slowest rank's time."""
+    measure); aggregate = all ranks' bytes / the slowest rank's time. bench:
+    anything with N, first and total_rec_bytes (an estimate is enough)."""
     if measure is None:
         from tools.host_path import measure
     avg = bench.total_rec_bytes / bench.N
@@ -1130,7 +1132,28 @@ def decode_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
     }
 
 
+class _Estimate:
+    """N, first and an estimate of the encoded bytes of this rank's records
+    (payload of a 4 K-record sample + ~1.1 KB of header and Metadata each),
+    for sizing the host-path leg before the bench allocates the device."""
+
+    def __init__(self, args, rank, world):
+        from honu_amd.workload import gen_totals
+        self.N = args.records
+        self.first, _ = weak_range(rank, world, args.records)
+        k = min(args.records, 4096)
+        pay = gen_totals(args.seed, args.shape, self.first, k)[3]
+        self.total_rec_bytes = int((pay / k + 1100) * self.N)
+
+
 def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
+    # the host-path leg first, on a device nothing else has touched yet
+    # (measured after the 250 GB of bench buffers were freed it ran at 28 GB/s
+    # instead of 46 for Large records)
+    host_path = None if args.no_host_path else host_path_leg(
+        _Estimate(args, rank, world), args, local, world, gather_max, all_ok)
+    gc.collect()
+    torch.cuda.empty_cache()
     bench = Bench(args, rank, local)
     for _ in range(args.warmup):
         bench.step()
@@ -1179,8 +1202,6 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
         scatter = scatter_leg(arena, off, dist, world, all_ok, gpu_parse_check(local),
                               torch.cuda.synchronize)
     bench.release()
-    host_path = None if args.no_host_path else host_path_leg(bench, args, local, world, gather_max,
-                                                             all_ok)
     decode = None if args.no_decode_legs else decode_legs(bench, args, world, barrier, gather_max,
                                                           all_ok)
     if rank != 0:

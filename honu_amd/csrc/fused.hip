@@ -214,11 +214,14 @@ struct SpecPub {
     }
 };
 
+// MODE 0: plain; 1: speculative publish; 2: guarded recovery (runs only when
+// the speculative launch before it raised misspec). Three instantiations, so
+// profiles tell the launches apart.
+template <int MODE>
 __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
-    DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t lb_words, int mode) {
-    // mode 0: plain; 1: speculative publish; 2: guarded recovery (runs only
-    // when the speculative launch before it raised misspec)
+    DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t lb_words) {
+    constexpr int mode = MODE;
     if (mode == 2 && __hip_atomic_load(&lb->misspec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
         return;  // every wave of the launch returns: the look-back state is untouched
     __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * FUSED_WAVE_BYTES];
@@ -421,16 +424,16 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
     // once gains less than the guarded launch costs (a 62 K-record Large chunk
     // 87.6 -> 91 us, profiles/r03/fused_spec_ab.jsonl)
     if (!FUSED_SPEC || tiles <= b * HONU_WAVES_PER_BLOCK) {
-        hipLaunchKernelGGL(k_decode_fused, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
-                           O, lb, lb_status, lb_words, 0);
+        hipLaunchKernelGGL(k_decode_fused<0>, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off,
+                           n, O, lb, lb_status, lb_words);
         return hipGetLastError();
     }
     // speculative launch, then the guarded recovery launch (a no-op unless a
     // record failed after publishing its counts: malformed input only)
-    hipLaunchKernelGGL(k_decode_fused, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
-                       O, lb, lb_status, lb_words, 1);
-    hipLaunchKernelGGL(k_decode_fused, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
-                       O, lb, lb_status, lb_words, 2);
+    hipLaunchKernelGGL(k_decode_fused<1>, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
+                       O, lb, lb_status, lb_words);
+    hipLaunchKernelGGL(k_decode_fused<2>, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
+                       O, lb, lb_status, lb_words);
     return hipGetLastError();
 }
 
