@@ -61,6 +61,9 @@ struct DecodeOut {
 #ifndef FUSED_SPEC
 #define FUSED_SPEC 1
 #endif
+#ifndef FUSED_EARLY_TICKET
+#define FUSED_EARLY_TICKET 1
+#endif
 #ifndef STAGE_SLOTS_N
 #define STAGE_SLOTS_N 1216
 #endif
@@ -138,10 +141,13 @@ struct AclStage {
     // the round's entries, from LDS, to the table (records whose ok is false
     // store nothing: capacity); lane e of a pass takes entry e of the round,
     // its list found as in issue()
-    HONU_DEV void store(const uint8_t *ws, honu_acl *__restrict__ acl, uint64_t ao, bool ok) const {
+    template <class AfterWait>
+    HONU_DEV void store(const uint8_t *ws, honu_acl *__restrict__ acl, uint64_t ao, bool ok,
+                        AfterWait after_wait) const {
         const uint32_t lane = lane_id();
         __builtin_amdgcn_s_waitcnt(0);  // the round's blocks have landed
         wave_sync();
+        after_wait();
         const bool in = lane >= r0 && lane < r1;
         uint32_t etot;
         const uint32_t epre = wave_excl32(in ? nacl : 0, etot);
@@ -240,11 +246,20 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     const bool stat_idx = stat || (O.dbg & 4);  // dbg 4: measurement only (with 2), static tiles at any size
     uint64_t k_static = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + threadIdx.x / HONU_WAVE;
     WSTAMP_START();
+    // ticket mode: the next tile's ticket is requested once the current tile's
+    // last ACL staging round has landed (its table stores and the rest of the
+    // tile then hide the atomic's round trip), or at the tile's end when it
+    // staged nothing (FUSED_EARLY_TICKET)
+    uint32_t tk = 0;
+    bool tk_pending = false;
     for (;;) {
         uint64_t t;
         if (stat_idx) {
             t = k_static;
             k_static += waves;
+        } else if (tk_pending) {
+            t = __builtin_amdgcn_readlane(tk, 0);
+            tk_pending = false;
         } else {
             t = lb_ticket(lb);
         }
@@ -380,7 +395,13 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         // bytes from LDS and stores the 20-byte row
         if (!(O.dbg & 1))
             while (S.more()) {
-                S.store(ws, O.acl, ao, ok);
+                const bool last = S.stop >= S.nbtot;  // wave-uniform
+                S.store(ws, O.acl, ao, ok, [&]() {
+                    if (FUSED_EARLY_TICKET && last && !stat_idx) {
+                        tk = lb_ticket_issue(lb);
+                        tk_pending = true;
+                    }
+                });
                 S.advance();
                 if (S.more()) S.issue(ws, rec);
             }

@@ -50,6 +50,15 @@ HONU_DEV uint32_t lb_epoch(LbState *s) {
     return uniform32(__hip_atomic_load(&s->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
+// The ticket atomic alone (lane 0's return value; read it with
+// readlane(v, 0) when needed, so its round trip overlaps other work).
+HONU_DEV uint32_t lb_ticket_issue(LbState *s) {
+    uint32_t t = 0;
+    if (lane_id() == 0)
+        t = __hip_atomic_fetch_add(&s->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return t;
+}
+
 // Next tile for this wave (wave-uniform).
 HONU_DEV uint64_t lb_ticket(LbState *s) {
     uint32_t t = 0;
