@@ -61,6 +61,16 @@ struct DecodeOut {
 #ifndef FUSED_SPEC
 #define FUSED_SPEC 1
 #endif
+// FUSED_SPEC_ACL: in speculative launches the walk takes every ACL list
+// that fits its record as all present without the flag gather; the fill,
+// which stages the list bytes anyway, checks the flags and raises misspec
+// (the guarded launch then redoes the batch) when one is not 1.
+#ifndef FUSED_SPEC_ACL
+#define FUSED_SPEC_ACL 1
+#endif
+#ifndef FUSED_SPEC_STATIC
+#define FUSED_SPEC_STATIC 0
+#endif
 #ifndef FUSED_EARLY_TICKET
 #define FUSED_EARLY_TICKET 1
 #endif
@@ -141,9 +151,11 @@ struct AclStage {
     // the round's entries, from LDS, to the table (records whose ok is false
     // store nothing: capacity); lane e of a pass takes entry e of the round,
     // its list found as in issue()
+    // returns true when an entry flag of the round is not 1 (checked only
+    // with chk: the walk speculated that every entry is present)
     template <class AfterWait>
-    HONU_DEV void store(const uint8_t *ws, honu_acl *__restrict__ acl, uint64_t ao, bool ok,
-                        AfterWait after_wait) const {
+    HONU_DEV bool store(const uint8_t *ws, honu_acl *__restrict__ acl, uint64_t ao, bool ok,
+                        bool chk, AfterWait after_wait) const {
         const uint32_t lane = lane_id();
         __builtin_amdgcn_s_waitcnt(0);  // the round's blocks have landed
         wave_sync();
@@ -154,6 +166,7 @@ struct AclStage {
         // per list: LDS offset of its first flag, table offset, capacity verdict
         const uint32_t lbase = 16 * (B - start) + (uint32_t)(apos & 15);
         const uint64_t tdst = ok ? ao : ~0ull;
+        bool bad = false;
         for (uint32_t w0 = 0; w0 < etot; w0 += HONU_WAVE) {  // wave-uniform
             const uint32_t r = (uint32_t)__builtin_popcountll(__ballot(epre <= w0)) - 1;
             uint32_t rp = __builtin_amdgcn_readlane(epre, r);
@@ -183,6 +196,8 @@ struct AclStage {
             window16(a, b, sft, lo, hi);
             const uint32_t bw = (sft >> 2) == 0 ? b.x : (sft >> 2) == 1 ? b.y : (sft >> 2) == 2 ? b.z : b.w;
             const uint32_t pm = (bw >> (8 * (sft & 3))) & 0xFF;
+            if (chk && e < etot)
+                bad |= ((const __attribute__((address_space(3))) uint8_t *)ws)[q - 1] != 1;
             if (e < etot && rt != ~0ull) {
                 uint32_t *d = reinterpret_cast<uint32_t *>(acl + rt + j);
                 d[0] = (uint32_t)lo;
@@ -193,6 +208,7 @@ struct AclStage {
             }
         }
         wave_sync();  // the LDS is the next round's (or the next tile's windows)
+        return bad;
     }
 };
 
@@ -204,6 +220,7 @@ struct AclStage {
 // speculation (it returns at once when the flag is clear).
 struct SpecPub {
     bool on;
+    bool spec_acl;  // the walk leaves the ACL entry flags to the fill (win.h NoEarly)
     uint64_t *status;
     uint64_t t;
     uint32_t ep;
@@ -278,6 +295,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
 #endif
         SpecPub early;
         early.on = mode == 1 && !(O.dbg & 2);
+        early.spec_acl = early.on && FUSED_SPEC_ACL;
         early.status = lb_status;
         early.t = t;
         early.ep = ep;
@@ -370,10 +388,13 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         // ACL table, lists the staging does not take (nil entries, or longer
         // than one round): the lane walks its list from global memory
         const uint64_t apos = P.acl_pos & GRP_POS_MASK;
+        bool acl_bad = false;  // spec_acl: an entry flag that is not 1
         if (ok && P.nacl && !S.staged()) {
             uint64_t p = apos;
+            const bool fast_list = (P.acl_pos & GRP_ACL_FAST) != 0;
             for (uint64_t k = 0; k < P.nacl; k++) {
                 uint32_t *d = reinterpret_cast<uint32_t *>(O.acl + ao + k);
+                if (early.spec_acl && fast_list && rec[p] != 1) acl_bad = true;
                 if (rec[p]) {
                     uint64_t lo, hi;
                     lane_fetch16(rec, p + 1, P.end, lo, hi);
@@ -396,7 +417,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         if (!(O.dbg & 1))
             while (S.more()) {
                 const bool last = S.stop >= S.nbtot;  // wave-uniform
-                S.store(ws, O.acl, ao, ok, [&]() {
+                acl_bad |= S.store(ws, O.acl, ao, ok, early.spec_acl, [&]() {
                     if (FUSED_EARLY_TICKET && last && !stat_idx) {
                         tk = lb_ticket_issue(lb);
                         tk_pending = true;
@@ -405,6 +426,14 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
                 S.advance();
                 if (S.more()) S.issue(ws, rec);
             }
+        // a speculated list had an entry that is not present (nil, or a bad
+        // flag): the walk read the fields after it at the wrong place. A
+        // record that failed after a speculated list is not filled, so its
+        // flags are unchecked: its failure may come from the speculation
+        // itself, so it counts as misspeculated too (malformed input only).
+        if (early.spec_acl && valid && P.st != HONU_OK && (P.acl_pos & GRP_ACL_FAST)) acl_bad = true;
+        if (early.spec_acl && __ballot(acl_bad) && lane == 0)
+            __hip_atomic_store(&lb->misspec, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         WSTAMP(13);  // ACL fill
     }
     lb_finish_blocks(lb, lb_status, lb_words, gridDim.x, &last_flag, mode == 2);
@@ -444,7 +473,7 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
     // waves: 1M Small 0.866 -> 0.840 ms); a launch whose tiles all start at
     // once gains less than the guarded launch costs (a 62 K-record Large chunk
     // 87.6 -> 91 us, profiles/r03/fused_spec_ab.jsonl)
-    if (!FUSED_SPEC || tiles <= b * HONU_WAVES_PER_BLOCK) {
+    if (!FUSED_SPEC || (!FUSED_SPEC_STATIC && tiles <= b * HONU_WAVES_PER_BLOCK)) {
         hipLaunchKernelGGL(k_decode_fused<0>, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off,
                            n, O, lb, lb_status, lb_words);
         return hipGetLastError();

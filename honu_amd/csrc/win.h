@@ -295,8 +295,13 @@ struct MemRow {
 
 // The walk's early hook (wave-uniform call, every lane): the record's ACL
 // entry and region counts once the regions are read (0 for a record that has
-// failed so far) and its aligned payload bytes. NoEarly: nothing.
+// failed so far) and its aligned payload bytes. spec_acl: the walk takes a
+// list that fits the record (18 bytes per entry) as all present WITHOUT
+// checking its entry flags; the caller must then check them (the fused
+// decode does, while it fills the table, and redoes the batch when one is
+// not 1). NoEarly: nothing, flags checked in the walk.
 struct NoEarly {
+    bool spec_acl = false;
     HONU_DEV void counts(uint64_t, uint64_t, uint64_t) {}
 };
 
@@ -479,7 +484,8 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
         fast = 18 * nacl <= D.end - D.p;
     }
     uint64_t ak = 0;
-    if (__ballot(fast)) {
+    const bool spec_acl = early.spec_acl;  // wave-uniform
+    if (!spec_acl && __ballot(fast)) {
         const uint64_t gbase = fast ? acl_pos : 0;
         const uint32_t gcnt = fast ? (uint32_t)(nacl < 64 ? nacl : 64) : 0;
         wave_sync();  // the windows' last reads are done
@@ -507,7 +513,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
         }
         wave_sync();  // the gather area becomes windows again
     }
-    {
+    if (!spec_acl) {
         bool chk = fast && ak < nacl;
         while (__ballot(chk)) {
             W.refill(chk ? ((D.p + 18 * ak) & ~15ull) : NOWIN);

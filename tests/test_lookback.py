@@ -186,3 +186,48 @@ def test_speculative_publish_recovers(oracle_lib, n, bad):
         good.check(oracle_lib, rec, off)
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("n,k", [(140000, 1), (140000, 200)])
+def test_speculative_acl_flags_recover(oracle_lib, n, k):
+    """Speculative launches also take every ACL list that fits its record as
+    all present without gathering its entry flags (fused.hip FUSED_SPEC_ACL);
+    the table fill checks them. Records whose lists hold nil entries (the walk
+    then read every later field at the wrong place) are spliced into a
+    2188-tile batch: the fill must raise misspec and the guarded launch redo
+    the batch bit-exact with the oracle; a clean batch decoded next on the same
+    context is exact too."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from corpora import random_metas
+    from honu_amd.metadata import pack_batch
+    rec, off, _ = oracle_lib.marshal_batch(gen_host_batch(43, "small", 0, n))
+    metas, datas = random_metas(4 * k + 40, 77)
+    pick = [i for i, m in enumerate(metas)
+            if m.ACL and any(a is None for a in m.ACL) and datas[i]][:k]
+    assert len(pick) == k
+    r2, o2, st2 = oracle_lib.marshal_batch(pack_batch([metas[i] for i in pick],
+                                                      [datas[i] for i in pick]))
+    assert (st2 == 0).all()
+    at = set(int(x) for x in np.linspace(3, n - 1, k).astype(np.int64))
+    pieces, noff, j = [], [0], 0
+    for i in range(n):
+        if i in at:
+            r = r2[int(o2[j]):int(o2[j + 1])]
+            j += 1
+        else:
+            r = rec[int(off[i]):int(off[i + 1])]
+        pieces.append(r)
+        noff.append(noff[-1] + len(r))
+    brec, boff = np.concatenate(pieces), np.array(noff, np.uint64)
+    c = hobj.Codec(0, n)
+    try:
+        hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
+        d = _Dec(c, brec, boff)
+        assert d() == 0
+        d.check(oracle_lib, brec, boff)
+        good = _Dec(c, rec, off)
+        assert good() == 0
+        good.check(oracle_lib, rec, off)
+    finally:
+        c.close()

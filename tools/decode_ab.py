@@ -58,11 +58,18 @@ def child(a):
         E = lambda nb: torch.empty(int(nb), dtype=torch.uint8, device=dev)  # noqa: E731
         dmeta, dinfo, dacl, dreg, tot = E(352 * n), E(32 * n), E(20 * acl_cap), E(4 * reg_cap), E(32)
         scrub = E(1 << 30) if a.cold else None
+        data_cap = total + 16 * n
+        data = E(data_cap) if a.what == "mat" else None
 
         def once():
             if a.what == "encode":  # header/tail encoder (honu_encode_records), payload copy apart
                 _lib.check(L.honu_encode_records(c, P(dm), P(dv), P(da), P(dr), P(do), n, P(rec),
                                                  total, P(oo), P(st), s), "encode_records")
+                return
+            if a.what == "mat":  # materialising: single-launch decode, then the copy kernel
+                _lib.check(L.honu_decode_records(c, P(rec), P(oo), n, P(dmeta), P(dinfo), P(dacl),
+                                                 acl_cap, P(dreg), reg_cap, 1, data_cap, P(tot), s), "dec")
+                _lib.check(L.honu_decode_payloads(c, P(rec), n, P(dinfo), P(data), P(tot), s), "copy")
                 return
             _lib.check(L.honu_decode_batch(c, P(rec), P(oo), n, P(dmeta), P(dinfo), P(dacl), acl_cap,
                                            P(dreg), reg_cap, 0, 0, P(tot), s), "decode")
@@ -81,7 +88,7 @@ def child(a):
         out_lines.append({"what": a.what, "workload": wl, "ms_median": ms[len(ms) // 2], "ms_min": ms[0],
                           "records_per_s": n / (ms[len(ms) // 2] / 1e3)})
         codec.close()
-        del rec, dmeta, dinfo, dacl, dreg, scrub
+        del rec, dmeta, dinfo, dacl, dreg, scrub, data
         torch.cuda.empty_cache()
     print(json.dumps(out_lines), flush=True)
 
@@ -93,7 +100,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--reps", type=int, default=9)
     ap.add_argument("--cold", action="store_true", help="1 GiB write before every launch")
-    ap.add_argument("--what", choices=["decode", "encode"], default="decode")
+    ap.add_argument("--what", choices=["decode", "encode", "mat"], default="decode",
+                    help="decode: zero copy; encode: header/tail encoder; mat: materialising "
+                         "decode (single launch + copy kernel)")
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
     if a.child:
