@@ -68,8 +68,13 @@ struct DecodeOut {
 #ifndef FUSED_SPEC_ACL
 #define FUSED_SPEC_ACL 1
 #endif
-#ifndef FUSED_SPEC_STATIC
-#define FUSED_SPEC_STATIC 0
+// launches of at least this many tiles speculate (publish + ACL flags) and
+// are followed by the guarded launch: with the flag gather gone the
+// speculation pays from ~1000 tiles also with static tiles (62 K Large
+// records 0.0876 -> 0.0825 ms, 64 K Small 0.092 -> 0.084; 512 tiles of Medium
+// 0.0706 -> 0.0722: the guarded launch's ~4 us weighs more there)
+#ifndef FUSED_SPEC_MIN_TILES
+#define FUSED_SPEC_MIN_TILES 768
 #endif
 #ifndef FUSED_EARLY_TICKET
 #define FUSED_EARLY_TICKET 1
@@ -469,11 +474,11 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
     const int dbg = 0;
 #endif
     DecodeOut O{meta, info, acl, acl_cap, reg, reg_cap, data_cap, materialize, scratch, offs, totals, dbg};
-    // speculation pays where tiles queue for tickets (more tiles than resident
-    // waves: 1M Small 0.866 -> 0.840 ms); a launch whose tiles all start at
-    // once gains less than the guarded launch costs (a 62 K-record Large chunk
-    // 87.6 -> 91 us, profiles/r03/fused_spec_ab.jsonl)
-    if (!FUSED_SPEC || (!FUSED_SPEC_STATIC && tiles <= b * HONU_WAVES_PER_BLOCK)) {
+    // speculation pays where tiles queue for tickets (1M Small 0.866 -> 0.840
+    // ms with the publish alone, -> 0.778 with the ACL flags too) and, since
+    // the flag gather is gone, in static-tile launches of ~1000 tiles and more
+    // (profiles/r03/fused_spec_ab.jsonl, spec_acl_ab*.jsonl)
+    if (!FUSED_SPEC || tiles < FUSED_SPEC_MIN_TILES) {
         hipLaunchKernelGGL(k_decode_fused<0>, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off,
                            n, O, lb, lb_status, lb_words);
         return hipGetLastError();
