@@ -93,6 +93,11 @@ struct SpanSegments {
 };
 
 #define SMALL_SEG_WAVES_FACTOR 4
+// average segment bytes from which a launch uses 1 / SMALL_SEG_WAVES_FACTOR of
+// its waves
+#ifndef COPY_FEW_WAVES_MIN
+#define COPY_FEW_WAVES_MIN (64u << 10)
+#endif
 
 template <class Seg, int UNROLL, int NT>
 __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t n,
@@ -104,7 +109,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t 
     // Large segments stream best from few waves (DRAM rows stay open: 2 WG per
     // CU measured best); short segments are latency bound and want every wave
     // the launch has (SMALL_SEG_WAVES_FACTOR x more).
-    if (n && total / n >= (64u << 10)) W /= SMALL_SEG_WAVES_FACTOR;
+    if (n && total / n >= COPY_FEW_WAVES_MIN) W /= SMALL_SEG_WAVES_FACTOR;
     if (w >= W) return;
     const uint64_t lo = base + ((total * w / W) & ~15ull);
     const uint64_t hi = (w + 1 == W) ? base + total : base + ((total * (w + 1) / W) & ~15ull);

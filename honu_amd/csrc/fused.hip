@@ -79,6 +79,23 @@ struct DecodeOut {
 #ifndef FUSED_EARLY_TICKET
 #define FUSED_EARLY_TICKET 1
 #endif
+// FUSED_STATIC_ALL: static tiles (tile t to wave t mod waves, no tickets) at
+// every batch size, not only when every tile has a resident wave of its own;
+// FUSED_PREFETCH: with static tiles a wave knows its next tile, so it loads
+// that tile's bounds after the walk and its header blocks after the look-back
+// wait, under the table fill, instead of at the top of the next tile
+// FUSED_WG_TICKET: in ticket mode a workgroup takes the first tiles of its
+// waves with one atomic (4 tickets), so a launch starts with 512 ticket
+// atomics on the one address instead of 2,048
+#ifndef FUSED_WG_TICKET
+#define FUSED_WG_TICKET 1
+#endif
+#ifndef FUSED_STATIC_ALL
+#define FUSED_STATIC_ALL 0
+#endif
+#ifndef FUSED_PREFETCH
+#define FUSED_PREFETCH 0
+#endif
 #ifndef STAGE_SLOTS_N
 #define STAGE_SLOTS_N 1216
 #endif
@@ -254,6 +271,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         return;  // every wave of the launch returns: the look-back state is untouched
     __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * FUSED_WAVE_BYTES];
     __shared__ uint32_t last_flag;
+    __shared__ uint32_t wg_ticket;
     uint8_t *ws = smem + (threadIdx.x / HONU_WAVE) * FUSED_WAVE_BYTES;
     const uint32_t lane = lane_id();
     const uint32_t ep = lb_epoch(lb);
@@ -265,7 +283,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     // look-back wait, to overlap them with it, doubled the wait: tiles are
     // then handed out ~40 us before their waves start them, which spreads the
     // publish times of consecutive tiles)
-    const bool stat_idx = stat || (O.dbg & 4);  // dbg 4: measurement only (with 2), static tiles at any size
+    const bool stat_idx = stat || FUSED_STATIC_ALL || (O.dbg & 4);  // dbg 4: measurement only (with 2), static tiles at any size
     uint64_t k_static = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + threadIdx.x / HONU_WAVE;
     WSTAMP_START();
     // ticket mode: the next tile's ticket is requested once the current tile's
@@ -274,6 +292,16 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     // staged nothing (FUSED_EARLY_TICKET)
     uint32_t tk = 0;
     bool tk_pending = false;
+    if (FUSED_WG_TICKET && !stat_idx) {  // wave-uniform, and the same in every wave of the workgroup
+        if (threadIdx.x == 0)
+            wg_ticket = __hip_atomic_fetch_add(&lb->ticket, (uint32_t)HONU_WAVES_PER_BLOCK, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        tk = wg_ticket + threadIdx.x / HONU_WAVE;
+        tk_pending = true;
+    }
+    TileHead Hn;  // FUSED_PREFETCH: the next static tile's head
+    bool have_next = false;
     for (;;) {
         uint64_t t;
         if (stat_idx) {
@@ -289,8 +317,12 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         const uint64_t i0 = t * HONU_WAVE, i = i0 + lane;
         const bool valid = i < n;
         TileHead H;
-        tile_head_bounds(i0, rec_off, n, H);
-        tile_head_bytes(rec, H);
+        if (FUSED_PREFETCH && have_next) {
+            H = Hn;
+        } else {
+            tile_head_bounds(i0, rec_off, n, H);
+            tile_head_bytes(rec, H);
+        }
         WinParse P;
 #if FUSED_MEMROW
         MemRow R;
@@ -329,6 +361,9 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
 #if !FUSED_MEMROW
         rows_out(ws, R, i0, n, O.meta);
 #endif
+        const bool pf = FUSED_PREFETCH && stat_idx && k_static < ntiles;  // wave-uniform
+        have_next = pf;
+        if (pf) tile_head_bounds(k_static * HONU_WAVE, rec_off, n, Hn);
         // the ACL lists with every entry present go to the table from LDS: the
         // first round of their blocks is staged now, before the wait, as it
         // needs no offsets
@@ -342,6 +377,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         } else {
             lb_resolve<3>(lb_status, t, ep, agg, excl);
         }
+        if (pf) tile_head_bytes(rec, Hn);
         WSTAMP(11);  // look-back wait
         if (t == ntiles - 1 && lane < 3)
             O.totals[lane] = lane == 0 ? excl[0] + agg[0] : (lane == 1 ? excl[1] + agg[1] : excl[2] + agg[2]);

@@ -33,6 +33,9 @@ def child(a):
         n = int(n)
         codec = Codec(0, n)
         L, c = codec.lib, codec.ctx
+        if a.lane_blocks_per_cu:  # grid of the single-launch decode (workgroups per CU)
+            ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+            _lib.check(L.honu_ctx_set_param(c, b"lane_blocks", a.lane_blocks_per_cu * ncu), "param")
         meta, var, acl, reg, off = gen_meta(1, shape, 0, n)
 
         def D(x):
@@ -103,6 +106,7 @@ def main():
     ap.add_argument("--what", choices=["decode", "encode", "mat"], default="decode",
                     help="decode: zero copy; encode: header/tail encoder; mat: materialising "
                          "decode (single launch + copy kernel)")
+    ap.add_argument("--lane-blocks-per-cu", type=int, default=0)
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
     if a.child:
@@ -110,10 +114,12 @@ def main():
         return
     libs = [x for x in a.libs.split(",") if x]
     for r in range(a.rounds):
-        for lib in libs:
-            env = dict(os.environ, HONU_LIB_PATH=os.path.abspath(lib))
+        for lib in libs:  # PATH or PATH@K: K workgroups per CU for the single-launch decode
+            path, _, lbk = lib.partition("@")
+            env = dict(os.environ, HONU_LIB_PATH=os.path.abspath(path))
             cmd = [sys.executable, os.path.abspath(__file__), "--child", "--workloads", a.workloads,
-                   "--reps", str(a.reps), "--what", a.what] + (["--cold"] if a.cold else [])
+                   "--reps", str(a.reps), "--what", a.what] + (["--cold"] if a.cold else []) + \
+                (["--lane-blocks-per-cu", lbk] if lbk else [])
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
             if p.returncode:
                 print(json.dumps({"round": r, "lib": lib, "error": p.stderr[-2000:]}), flush=True)
