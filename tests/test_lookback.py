@@ -231,3 +231,39 @@ def test_speculative_acl_flags_recover(oracle_lib, n, k):
         good.check(oracle_lib, rec, off)
     finally:
         c.close()
+
+
+def test_concurrent_ticket_and_static_launches_on_two_streams(oracle_lib):
+    """Two contexts decoding at once on their own streams: ticket-mode launches
+    (2188 tiles: a workgroup takes its waves' first tiles with one atomic,
+    fused.hip FUSED_WG_TICKET) beside each other and beside a static-tile
+    launch. Each launch's grid fills the chip, so neither is resident at once;
+    a wave only ever waits on tiles that running waves hold (tickets are taken
+    by running waves, static tiles wait only on lower-numbered workgroups), so
+    every launch completes, bit-exact."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    n_ticket, n_static = 140000, 64 * (2 * 4 * ncu) - 17
+    b1 = oracle_lib.marshal_batch(gen_host_batch(51, "small", 0, n_ticket))
+    b2 = oracle_lib.marshal_batch(gen_host_batch(52, "small", 0, n_ticket))
+    b3 = oracle_lib.marshal_batch(gen_host_batch(53, "small", 0, n_static))
+    c1, c2 = hobj.Codec(0, n_ticket), hobj.Codec(0, n_ticket)
+    try:
+        d1, d2, d3 = _Dec(c1, *b1[:2]), _Dec(c2, *b2[:2]), _Dec(c2, *b3[:2])
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        torch.cuda.synchronize()
+        for _ in range(3):
+            with torch.cuda.stream(s1):
+                assert d1() == 0
+                assert d1() == 0
+            with torch.cuda.stream(s2):
+                assert d2() == 0  # beside d1's first launch
+                assert d3() == 0  # static tiles, beside d1's second launch
+            torch.cuda.synchronize()
+        d1.check(oracle_lib, *b1[:2])
+        d2.check(oracle_lib, *b2[:2])
+        d3.check(oracle_lib, *b3[:2])
+    finally:
+        c1.close()
+        c2.close()
