@@ -76,6 +76,11 @@ def parse_args(argv=None):
                         "beside them (0 = no cap; -1 = auto: 2 when records average > 64 KiB, "
                         "where the copies dominate, else no cap)")
     p.add_argument("--copy-prio", type=int, default=1, help="copy stream gets high priority")
+    p.add_argument("--meta-cu-stride", type=int, default=0,
+                   help="metadata kernels on the CUs i with i %% S == 0 only (a CU-masked stream); "
+                        "0: every CU")
+    p.add_argument("--copy-cu-mask", choices=["all", "rest"], default="rest",
+                   help="with --meta-cu-stride: the copy stream on every CU or on the others only")
     p.add_argument("--encode-copy-after", choices=["scan", "meta"], default="scan",
                    help="start a chunk's encode payload copy after its sizes + scan, or after "
                         "its header/tail encoder too")
@@ -211,6 +216,11 @@ class Bench:
         # payload copies: the bandwidth-bound critical path, dispatched first
         self.sc = (torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio else 0)
                    if nslots == 2 else self.sm)
+        if args.meta_cu_stride and nslots == 2:  # metadata and copies on their own CUs
+            S = args.meta_cu_stride
+            self.sm = cu_masked_stream(self.dev, ncu, lambda i: i % S == 0)
+            if args.copy_cu_mask == "rest":
+                self.sc = cu_masked_stream(self.dev, ncu, lambda i: i % S != 0)
         self.sv = torch.cuda.Stream(self.dev)  # verification of drained chunks
         self.events = None
         self.last = None
@@ -882,6 +892,24 @@ def cpu_baseline(args):
     }
 
 
+def cu_masked_stream(dev, ncu, use):
+    """A torch view of a HIP stream whose kernels run only on the CUs i with
+    use(i) (hipExtStreamCreateWithCUMask); the stream lives to process exit."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    words = (ncu + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for i in range(ncu):
+        if use(i):
+            mask[i // 32] |= 1 << (i % 32)
+    h = ctypes.c_void_p()
+    torch.cuda.set_device(dev)
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(words), mask)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask: {rc}")
+    return torch.cuda.ExternalStream(h.value, device=dev)
+
+
 def _free_port():
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
@@ -1243,6 +1271,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
             "meta_blocks_per_cu": 8 if (args.serial or not args.meta_blocks) else args.meta_blocks,
             "lane_blocks_per_cu": bench.lane_blocks or None,
             "copy_blocks_per_cu": args.copy_blocks or 2,
+            "meta_cu_stride": args.meta_cu_stride or None,
             "metadata_decode": "fused" if bench.fused_decode(bench.C) else "split",
         },
         "records_per_s": total_records / step_s,
