@@ -76,6 +76,10 @@ def parse_args(argv=None):
                         "beside them (0 = no cap; -1 = auto: 2 when records average > 64 KiB, "
                         "where the copies dominate, else no cap)")
     p.add_argument("--copy-prio", type=int, default=1, help="copy stream gets high priority")
+    p.add_argument("--meta-beside", choices=["auto", "encode", "decode"], default="auto",
+                   help="chunk k+1's metadata kernels start when its slot frees (beside chunk "
+                        "k's encode copy) or once chunk k's encode copy is done (beside its "
+                        "decode copy); auto: decode for records over 64 KiB on average")
     p.add_argument("--meta-cu-stride", type=int, default=0,
                    help="metadata kernels on the CUs i with i %% S == 0 only (a CU-masked stream); "
                         "0: every CU")
@@ -201,6 +205,12 @@ class Bench:
             # GiB/s capped at 4 per CU, profiles/r03/medium_lane_blocks_ab.txt)
             lane_blocks = 2 if avg > 65536 else 0
         self.lane_blocks = 0 if args.serial else lane_blocks
+        # measured (profiles/r03/ab/meta_beside_ab.txt): 1M Large 1343-1347 -> 1377 GiB/s and
+        # 1M Mixed 1194 -> 1213-1223 with the metadata beside the decode copy, 1M Medium
+        # 1052-1078 -> 1048-1061
+        self.meta_beside = args.meta_beside
+        if self.meta_beside == "auto":
+            self.meta_beside = "decode" if self.total_rec_bytes / N > 65536 else "encode"
         for sl in self.slots:
             if args.copy_blocks:
                 _lib.check(self.lib.honu_ctx_set_param(sl.codec.ctx, b"copy_blocks",
@@ -225,6 +235,7 @@ class Bench:
         self.events = None
         self.last = None
         self.nchunk = 0  # chunks issued so far, across steps: slots alternate globally
+        self.enc_done = None  # the last issued chunk's encode copy (--meta-beside decode)
         torch.cuda.synchronize()
 
     def _sizes(self, codec, a, b, out_off, status, s):
@@ -284,6 +295,8 @@ class Bench:
         c = sl.codec.ctx
         if sl.free is not None:
             sm.wait_event(sl.free)
+        if self.meta_beside == "decode" and self.enc_done is not None:
+            sm.wait_event(self.enc_done)
         ms = sm.cuda_stream
         self._sizes(sl.codec, a, b, sl.out_off, sl.status, ms)
         ev_off = torch.cuda.Event()
@@ -320,6 +333,8 @@ class Bench:
                                           cs), "encode_payloads")
         if timed:
             e1.record(sc)
+        self.enc_done = torch.cuda.Event()
+        self.enc_done.record(sc)
         sc.wait_event(ev_fill)
         e2 = torch.cuda.Event(enable_timing=True) if timed else None
         e3 = torch.cuda.Event(enable_timing=True) if timed else None
@@ -1272,6 +1287,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
             "lane_blocks_per_cu": bench.lane_blocks or None,
             "copy_blocks_per_cu": args.copy_blocks or 2,
             "meta_cu_stride": args.meta_cu_stride or None,
+            "metadata_beside": bench.meta_beside,
             "metadata_decode": "fused" if bench.fused_decode(bench.C) else "split",
         },
         "records_per_s": total_records / step_s,

@@ -36,13 +36,13 @@ def _gpu():
 
 
 @pytest.mark.parametrize("decode", ["fused", "split"])
-@pytest.mark.parametrize("after", ["scan", "meta"])
+@pytest.mark.parametrize("after,beside", [("scan", "encode"), ("meta", "encode"), ("scan", "decode")])
 @pytest.mark.parametrize("shape,n", [("small", 4000), ("mixed", 1200), ("large", 160)])
-def test_bench_pipeline_bit_exact(oracle_lib, shape, n, after, decode):
+def test_bench_pipeline_bit_exact(oracle_lib, shape, n, after, decode, beside):
     seed = 7
     args = bench.parse_args(["--records", str(n), "--shape", shape, "--min-chunks", "5",
                              "--encode-copy-after", after, "--seed", str(seed),
-                             "--decode", decode])
+                             "--decode", decode, "--meta-beside", beside])
     b = bench.Bench(args, 0, 0)
     assert len(b.chunks) >= 5 and len(b.slots) == 2
     hb = gen_host_batch(seed, shape, 0, n)  # the same records the device generator made
