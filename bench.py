@@ -357,8 +357,12 @@ class Bench:
     FUSED_DECODE_MIN = 128 << 10
 
     def fused_decode(self, n):
+        # beside the decode copy the persistent single-launch grid costs the copy more
+        # than it saves: 1M Mixed (262 K-record chunks) 1143-1146 GiB/s fused vs
+        # 1267-1269 split (profiles/r03/ab/meta_beside_decode_form_ab.txt)
         d = self.args.decode
-        return d == "fused" or (d == "auto" and n >= self.FUSED_DECODE_MIN)
+        return d == "fused" or (d == "auto" and n >= self.FUSED_DECODE_MIN
+                                and self.meta_beside != "decode")
 
     def verify(self):
         """Every record of the batch, after the timed steps: one more pipelined
