@@ -79,17 +79,21 @@ struct DecodeOut {
 #ifndef FUSED_EARLY_TICKET
 #define FUSED_EARLY_TICKET 1
 #endif
-// FUSED_STATIC_ALL: static tiles (tile t to wave t mod waves, no tickets) at
-// every batch size, not only when every tile has a resident wave of its own;
-// FUSED_PREFETCH: with static tiles a wave knows its next tile, so it loads
-// that tile's bounds after the walk and its header blocks after the look-back
-// wait, under the table fill, instead of at the top of the next tile
 // FUSED_WG_TICKET: in ticket mode a workgroup takes the first tiles of its
 // waves with one atomic (4 tickets), so a launch starts with 512 ticket
-// atomics on the one address instead of 2,048
+// atomics on the one address instead of 2,048 (1M Small 0.780 -> 0.757 ms,
+// 262 K Large 0.258 -> 0.238 ms, profiles/r03/ab/wg_ticket_ab.jsonl)
 #ifndef FUSED_WG_TICKET
 #define FUSED_WG_TICKET 1
 #endif
+// Measurement only (variant libraries, tools/variant_lib.sh), never in a
+// product build:
+// FUSED_STATIC_ALL: static tiles (tile t to wave t mod waves, no tickets) at
+// every batch size. Faster (262 K Large 0.231 ms) but NOT deadlock-free: a
+// wave's second tile waits on tiles of higher-numbered workgroups, which need
+// not be resident, so two such launches on two streams can each hold the CUs
+// the other waits for. FUSED_PREFETCH (with static tiles): the next tile's
+// bounds and header loaded under the table fill; measured no change.
 #ifndef FUSED_STATIC_ALL
 #define FUSED_STATIC_ALL 0
 #endif
