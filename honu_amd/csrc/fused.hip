@@ -100,6 +100,12 @@ struct DecodeOut {
 #ifndef FUSED_PREFETCH
 #define FUSED_PREFETCH 0
 #endif
+// FILL_DW: the table fill reads an entry as five aligned dwords (1M Small
+// 0.760 -> 0.747 ms, a 62 K Large chunk 85.8 -> 82.8 us,
+// profiles/r03/ab/fill_dw_ab.jsonl); 0: two 16-byte reads and window16
+#ifndef FILL_DW
+#define FILL_DW 1
+#endif
 #ifndef STAGE_SLOTS_N
 #define STAGE_SLOTS_N 1216
 #endif
@@ -215,13 +221,26 @@ struct AclStage {
             const uint32_t j = e - rp;
             // the ClientID's first byte in LDS, Permissions 16 bytes on
             const uint32_t q = rl + 18 * j + 1;
+            uint64_t lo, hi;
+            uint32_t pm;
+#if FILL_DW
+            // five aligned dwords and four v_alignbyte instead of two 16-byte
+            // reads and the per-lane select chain of window16
+            const uint32_t sh = q & 3u;
+            const __attribute__((address_space(3))) uint32_t *w =
+                (const __attribute__((address_space(3))) uint32_t *)(ws + (q & ~3u));
+            const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
+            lo = ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32) | __builtin_amdgcn_alignbyte(d1, d0, sh);
+            hi = ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, sh) << 32) | __builtin_amdgcn_alignbyte(d3, d2, sh);
+            pm = (d4 >> (8 * sh)) & 0xFF;
+#else
             const uint32_t qa = q & ~15u, sft = q & 15u;
             const u32x4 a = *reinterpret_cast<const u32x4 *>(ws + qa);
             const u32x4 b = *reinterpret_cast<const u32x4 *>(ws + qa + 16);
-            uint64_t lo, hi;
             window16(a, b, sft, lo, hi);
             const uint32_t bw = (sft >> 2) == 0 ? b.x : (sft >> 2) == 1 ? b.y : (sft >> 2) == 2 ? b.z : b.w;
-            const uint32_t pm = (bw >> (8 * (sft & 3))) & 0xFF;
+            pm = (bw >> (8 * (sft & 3))) & 0xFF;
+#endif
             if (chk && e < etot)
                 bad |= ((const __attribute__((address_space(3))) uint8_t *)ws)[q - 1] != 1;
             if (e < etot && rt != ~0ull) {
