@@ -28,6 +28,14 @@ namespace honu {
 
 #define GO_MAX_ALLOC (1ull << 48)  // runtime maxAlloc, linux/amd64
 
+// WIN_MIRROR: the pad slot of every window holds a copy of ring slot 0, so a
+// 16-byte field read is five aligned dword reads with no wrap and four
+// v_alignbyte, not two 16-byte reads and a per-lane select chain (1M Small
+// zero copy 0.751 -> 0.736 ms, 262 K Large 239 -> 234 us, split parse of 16 K
+// Small 63.2 -> 61.8 us; profiles/r03/ab/win_mirror_ab.jsonl)
+#ifndef WIN_MIRROR
+#define WIN_MIRROR 1
+#endif
 constexpr uint32_t WB = 256;           // window bytes per lane (16 blocks)
 constexpr uint32_t WSL = WB / 16 + 1;  // LDS stride in 16-byte slots: one pad slot per
                                        // window puts the lanes of a ds_read_b128 group
@@ -74,9 +82,15 @@ struct LaneWin {
             const uint32_t s = 64 * k + lane;
             const uint32_t L = s / WSL, c = s % WSL;
             const uint64_t b = wants[L];
+#if WIN_MIRROR
+            if (b != NOWIN) {  // slot 16 mirrors ring slot 0 (fetch16 reads across the wrap)
+                const uint64_t w0 = b >> 4;
+                const uint64_t blk = w0 + (((c & 15) - w0) & 15);  // the block of [w0, w0+16) in slot c
+#else
             if (c < WB / 16 && b != NOWIN) {
                 const uint64_t w0 = b >> 4;
                 const uint64_t blk = w0 + ((c - w0) & 15);  // the block of [w0, w0+16) in slot c
+#endif
                 const uint64_t o = olds[L];
                 const bool held = o != NOWIN && blk >= (o >> 4) && blk < (o >> 4) + 16;
                 if (!held && 16 * blk < lims[L])
@@ -101,6 +115,21 @@ struct LaneWin {
         return ((const __attribute__((address_space(1))) uint8_t *)rec)[p];
     }
     HONU_DEV void fetch16(uint64_t p, uint64_t end, uint64_t &lo, uint64_t &hi) const {
+#if WIN_MIRROR
+        if (wb != NOWIN && p >= wb && p - wb <= WB - 16) {
+            // [p, p + 16) as five aligned dwords of the lane's slots (slot 16
+            // mirrors slot 0, so the run never wraps) and four v_alignbyte
+            const uint32_t o = ((uint32_t)(p >> 4) & 15) * 16 + (uint32_t)(p & 15);
+            const uint32_t sh = o & 3;
+            const __attribute__((address_space(3))) uint32_t *w =
+                (const __attribute__((address_space(3))) uint32_t *)(mine() + (o & ~3u));
+            const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
+            lo = ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32) | __builtin_amdgcn_alignbyte(d1, d0, sh);
+            hi = ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, sh) << 32) | __builtin_amdgcn_alignbyte(d3, d2, sh);
+            return;
+        }
+        lane_fetch16(rec, p, end, lo, hi);
+#else
         if (wb != NOWIN && p >= wb && p - wb <= WB - 16) {
             const uint64_t blk = p >> 4;
             const u32x4 a = *reinterpret_cast<const u32x4 *>(slot(blk));
@@ -109,6 +138,7 @@ struct LaneWin {
         } else {
             lane_fetch16(rec, p, end, lo, hi);
         }
+#endif
     }
 };
 
