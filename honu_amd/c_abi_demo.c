@@ -5,14 +5,20 @@
  * pointers, sizes and the null stream. Built by honu_amd/Makefile; run by
  * tests/test_c_abi.py on a GPU box.
  *
- *   c_abi_demo [shape] [n]   shape: 0 Small, 1 Medium, 2 Large, 4 Mixed
+ *   c_abi_demo [shape] [n] [dump_dir]   shape: 0 Small, 1 Medium, 2 Large, 4 Mixed
  *
  * Steps: generate a synthetic host batch (rows, var arena, ACL and region
  * tables, payloads) -> H2D -> honu_marshal_batch -> D2H of offsets/records ->
- * honu_decode_batch (zero copy) -> D2H of rows/info -> honu_decode_batch
+ * honu_decode_batch (zero copy) with ACL / region tables sized from COUNTS,
+ * not record bytes: a first call with small caps, the totals it reports
+ * (d_totals: the entries the batch needs), tables re-allocated to exactly
+ * those and a second call -> D2H of rows/info/tables -> honu_decode_batch
  * materialising -> D2H of payloads; checks every status, the decoded rows'
- * scalar fields against the input rows and every payload's digest. Exit 0 and
- * one "ok" line on success.
+ * scalar fields against the input rows and every payload's digest. With
+ * dump_dir, the records arena, offsets and the zero-copy outputs are written
+ * there (rec.bin, off.bin, meta.bin, info.bin, acl.bin, reg.bin, tot.bin) for
+ * tests/test_c_abi.py to compare with the oracle. Exit 0 and one "ok" line on
+ * success.
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -38,6 +44,15 @@
         }                                                                \
     } while (0)
 
+static int dump(const char *dir, const char *name, const void *p, uint64_t bytes) {
+    char path[4096];
+    snprintf(path, sizeof path, "%s/%s", dir, name);
+    FILE *f = fopen(path, "wb");
+    if (!f) return 1;
+    const int bad = bytes && fwrite(p, 1, bytes, f) != bytes;
+    return fclose(f) != 0 || bad;
+}
+
 static void *h2d(const void *h, uint64_t bytes) {
     void *d = honu_device_alloc(bytes + 16);
     if (d && bytes && honu_memcpy_h2d(d, h, bytes, NULL) != HONU_OK) return NULL;
@@ -47,6 +62,7 @@ static void *h2d(const void *h, uint64_t bytes) {
 int main(int argc, char **argv) {
     const int32_t shape = argc > 1 ? atoi(argv[1]) : HONU_SHAPE_SMALL;
     const uint64_t n = argc > 2 ? strtoull(argv[2], NULL, 10) : 4096;
+    const char *dump_dir = argc > 3 ? argv[3] : NULL;
     const uint64_t seed = 12345;
     int32_t err = 0;
     honu_ctx *ctx = honu_ctx_create(0, n, &err);
@@ -93,23 +109,70 @@ int main(int argc, char **argv) {
             return 1;
         }
     const uint64_t rec_bytes = off[n];
-    /* 4. Metadata() + zero-copy Data(), then a materialising decode */
+    /* 4. Metadata() + zero-copy Data(), then a materialising decode. The ACL
+     * and region tables are sized by the batch's entry counts: a first call
+     * with small caps (one entry per record here, so the retry always runs;
+     * a binding would start from its typical counts) reports the totals in
+     * d_totals (records past the caps get HONU_ERR_CAPACITY), the tables are
+     * re-allocated to exactly the totals and the call is repeated. Sizing them
+     * by record bytes instead (an entry takes >= 1 byte) would allocate
+     * 20 + 4 bytes per RECORD BYTE: 24x the records arena. */
     honu_meta *d_meta = (honu_meta *)honu_device_alloc(sizeof(honu_meta) * n);
     honu_record_info *d_info = (honu_record_info *)honu_device_alloc(sizeof(honu_record_info) * n);
-    honu_acl *d_tacl = (honu_acl *)honu_device_alloc(sizeof(honu_acl) * rec_bytes + 16);
-    uint32_t *d_treg = (uint32_t *)honu_device_alloc(4 * rec_bytes + 16);
     uint64_t *d_tot = (uint64_t *)honu_device_alloc(32);
+    NEED(d_meta && d_info && d_tot);
+    uint64_t acl_cap = n, reg_cap = n, totals[4] = {0, 0, 0, 0};
+    honu_acl *d_tacl = NULL;
+    uint32_t *d_treg = NULL;
+    int calls = 0;
+    for (;;) {
+        d_tacl = (honu_acl *)honu_device_alloc(sizeof(honu_acl) * acl_cap + 16);
+        d_treg = (uint32_t *)honu_device_alloc(4 * reg_cap + 16);
+        NEED(d_tacl && d_treg);
+        CHECK(honu_decode_batch(ctx, d_out, d_off, n, d_meta, d_info, d_tacl, acl_cap, d_treg, reg_cap,
+                                NULL, 0, d_tot, NULL));
+        calls++;
+        CHECK(honu_memcpy_d2h(totals, d_tot, 24, NULL));
+        CHECK(honu_stream_sync(NULL));
+        if (totals[0] <= acl_cap && totals[1] <= reg_cap) break;
+        if (calls == 2) {
+            fprintf(stderr, "totals grew between two decodes of one batch\n");
+            return 1;
+        }
+        honu_device_free(d_tacl);
+        honu_device_free(d_treg);
+        acl_cap = totals[0];
+        reg_cap = totals[1];
+    }
+    const uint64_t table_bytes = sizeof(honu_acl) * acl_cap + 4 * reg_cap;
     const uint64_t data_cap = rec_bytes + 16 * n;
     uint8_t *d_data = (uint8_t *)honu_device_alloc(data_cap);
-    NEED(d_meta && d_info && d_tacl && d_treg && d_tot && d_data);
-    CHECK(honu_decode_batch(ctx, d_out, d_off, n, d_meta, d_info, d_tacl, rec_bytes, d_treg,
-                            rec_bytes, NULL, 0, d_tot, NULL));
+    NEED(d_data);
     honu_meta *meta = (honu_meta *)honu_host_alloc(sizeof(honu_meta) * n);
     honu_record_info *info = (honu_record_info *)honu_host_alloc(sizeof(honu_record_info) * n);
-    NEED(meta && info);
+    honu_acl *tacl = (honu_acl *)honu_host_alloc(sizeof(honu_acl) * acl_cap + 16);
+    uint32_t *treg = (uint32_t *)honu_host_alloc(4 * reg_cap + 16);
+    NEED(meta && info && tacl && treg);
     CHECK(honu_memcpy_d2h(meta, d_meta, sizeof(honu_meta) * n, NULL));
     CHECK(honu_memcpy_d2h(info, d_info, sizeof(honu_record_info) * n, NULL));
+    CHECK(honu_memcpy_d2h(tacl, d_tacl, sizeof(honu_acl) * totals[0], NULL));
+    CHECK(honu_memcpy_d2h(treg, d_treg, 4 * totals[1], NULL));
     CHECK(honu_stream_sync(NULL));
+    if (dump_dir) {
+        uint8_t *rec = (uint8_t *)honu_host_alloc(rec_bytes + 16);
+        NEED(rec);
+        CHECK(honu_memcpy_d2h(rec, d_out, rec_bytes, NULL));
+        CHECK(honu_stream_sync(NULL));
+        if (dump(dump_dir, "rec.bin", rec, rec_bytes) || dump(dump_dir, "off.bin", off, 8 * (n + 1)) ||
+            dump(dump_dir, "meta.bin", meta, sizeof(honu_meta) * n) ||
+            dump(dump_dir, "info.bin", info, sizeof(honu_record_info) * n) ||
+            dump(dump_dir, "acl.bin", tacl, sizeof(honu_acl) * totals[0]) ||
+            dump(dump_dir, "reg.bin", treg, 4 * totals[1]) || dump(dump_dir, "tot.bin", totals, 24)) {
+            fprintf(stderr, "cannot write %s\n", dump_dir);
+            return 1;
+        }
+        honu_host_free(rec);
+    }
     for (uint64_t i = 0; i < n; i++) {
         const honu_meta *a = rows + i, *b = meta + i;
         if (info[i].meta_status != HONU_OK || info[i].data_status != HONU_OK ||
@@ -121,8 +184,8 @@ int main(int argc, char **argv) {
             return 1;
         }
     }
-    CHECK(honu_decode_batch(ctx, d_out, d_off, n, d_meta, d_info, d_tacl, rec_bytes, d_treg,
-                            rec_bytes, d_data, data_cap, d_tot, NULL));
+    CHECK(honu_decode_batch(ctx, d_out, d_off, n, d_meta, d_info, d_tacl, acl_cap, d_treg,
+                            reg_cap, d_data, data_cap, d_tot, NULL));
     uint8_t *data = (uint8_t *)honu_host_alloc(data_cap);
     NEED(data);
     CHECK(honu_memcpy_d2h(info, d_info, sizeof(honu_record_info) * n, NULL));
@@ -136,8 +199,10 @@ int main(int argc, char **argv) {
             return 1;
         }
     }
-    printf("ok: %llu records, %llu encoded bytes, marshal + decode + materialise through the C ABI\n",
-           (unsigned long long)n, (unsigned long long)rec_bytes);
+    printf("ok: %llu records, %llu encoded bytes, marshal + decode + materialise through the C ABI; "
+           "decode calls %d, table bytes %llu (ACL entries %llu, regions %llu)\n",
+           (unsigned long long)n, (unsigned long long)rec_bytes, calls, (unsigned long long)table_bytes,
+           (unsigned long long)totals[0], (unsigned long long)totals[1]);
     honu_ctx_destroy(ctx);
     return 0;
 }

@@ -10,8 +10,6 @@
 // writes every output with those offsets — rows once, region ids from
 // registers, ACL entries re-read right after the walk — with no scratch round
 // trips and no launch boundaries.
-#include <stdlib.h>
-
 #include "lookback.h"
 #include "win.h"
 
@@ -36,76 +34,30 @@ struct DecodeOut {
     DecodeScratch *scratch;   // materialize: payload sources for honu_decode_payloads
     uint64_t *offs;           // materialize: offs[3i+2] = data arena offset
     uint64_t *totals;         // column totals (3)
-    int dbg;                  // A/B measurement knobs (HONU_FUSED_DBG): 1 no ACL fill,
-                              // 2 no look-back wait, 4 static tiles (with 2)
 };
+
+// Launches of at least this many tiles speculate (publish + ACL flags, below)
+// and are followed by the guarded launch: with the flag gather gone the
+// speculation pays from ~1000 tiles also with static tiles (62 K Large
+// records 0.0876 -> 0.0825 ms, 64 K Small 0.092 -> 0.084; 512 tiles of Medium
+// 0.0706 -> 0.0722: the guarded launch's ~4 us weighs more there).
+// Measured and not kept (sources in git history, commit 88edda1): rows stored
+// field by field during the walk (MemRow, 30 % slower: vmcnt counts stores,
+// so every window refill also waited for the row stores); static tiles at
+// every batch size (faster, but a wave's second tile would wait on tiles of
+// workgroups that need not be resident: not deadlock-free beside another
+// launch); the next static tile's head prefetched under the fill (no change);
+// ACL entries read as two 16-byte LDS reads and a select chain (FILL_DW 0,
+// slower); the measurement knobs that skip the fill, the look-back wait or
+// the tickets (HONU_FUSED_DBG). DESIGN §3 has the numbers.
+constexpr uint64_t FUSED_SPEC_MIN_TILES = 768;
 
 // The ACL lists (every entry present) of a tile staged into the wave's LDS
 // (its windows, free after the walk) for the table fill: round after round,
 // the aligned 16-byte blocks of a run of whole lists, up to STAGE_SLOTS blocks,
 // land by global_load_lds (one per-lane source block per slot, 1 KB per
 // instruction); the entries are then read from LDS. Lists of more than
-// STAGE_SLOTS blocks (over ~900 entries) are not staged.
-// FUSED_MEMROW 1: rows stored field by field during the walk (win.h MemRow)
-// instead of held in registers and written out through LDS afterwards. It
-// frees 81 VGPRs (244 -> 163, enough for 3 waves per SIMD) but measured 30 %
-// slower at the same occupancy (1M Small 0.856 -> 1.115 ms, a Large chunk
-// +3 %, profiles/r03/fused_memrow_ab.jsonl): vmcnt counts stores on gfx950,
-// so every window refill's wait also waits for the scattered row stores
-// issued before it (the walk's LDS-only stages doubled: fields to the ACL
-// count 7.3 -> 15.6 us per tile). Kept for measurement; the default holds
-// the row in registers.
-#ifndef FUSED_MEMROW
-#define FUSED_MEMROW 0
-#endif
-#ifndef FUSED_SPEC
-#define FUSED_SPEC 1
-#endif
-// FUSED_SPEC_ACL: in speculative launches the walk takes every ACL list
-// that fits its record as all present without the flag gather; the fill,
-// which stages the list bytes anyway, checks the flags and raises misspec
-// (the guarded launch then redoes the batch) when one is not 1.
-#ifndef FUSED_SPEC_ACL
-#define FUSED_SPEC_ACL 1
-#endif
-// launches of at least this many tiles speculate (publish + ACL flags) and
-// are followed by the guarded launch: with the flag gather gone the
-// speculation pays from ~1000 tiles also with static tiles (62 K Large
-// records 0.0876 -> 0.0825 ms, 64 K Small 0.092 -> 0.084; 512 tiles of Medium
-// 0.0706 -> 0.0722: the guarded launch's ~4 us weighs more there)
-#ifndef FUSED_SPEC_MIN_TILES
-#define FUSED_SPEC_MIN_TILES 768
-#endif
-#ifndef FUSED_EARLY_TICKET
-#define FUSED_EARLY_TICKET 1
-#endif
-// FUSED_WG_TICKET: in ticket mode a workgroup takes the first tiles of its
-// waves with one atomic (4 tickets), so a launch starts with 512 ticket
-// atomics on the one address instead of 2,048 (1M Small 0.780 -> 0.757 ms,
-// 262 K Large 0.258 -> 0.238 ms, profiles/r03/ab/wg_ticket_ab.jsonl)
-#ifndef FUSED_WG_TICKET
-#define FUSED_WG_TICKET 1
-#endif
-// Measurement only (variant libraries, tools/variant_lib.sh), never in a
-// product build:
-// FUSED_STATIC_ALL: static tiles (tile t to wave t mod waves, no tickets) at
-// every batch size. Faster (262 K Large 0.231 ms) but NOT deadlock-free: a
-// wave's second tile waits on tiles of higher-numbered workgroups, which need
-// not be resident, so two such launches on two streams can each hold the CUs
-// the other waits for. FUSED_PREFETCH (with static tiles): the next tile's
-// bounds and header loaded under the table fill; measured no change.
-#ifndef FUSED_STATIC_ALL
-#define FUSED_STATIC_ALL 0
-#endif
-#ifndef FUSED_PREFETCH
-#define FUSED_PREFETCH 0
-#endif
-// FILL_DW: the table fill reads an entry as five aligned dwords (1M Small
-// 0.760 -> 0.747 ms, a 62 K Large chunk 85.8 -> 82.8 us,
-// profiles/r03/ab/fill_dw_ab.jsonl); 0: two 16-byte reads and window16
-#ifndef FILL_DW
-#define FILL_DW 1
-#endif
+// STAGE_SLOTS blocks (over ~1,080 entries) are not staged.
 #ifndef STAGE_SLOTS_N
 #define STAGE_SLOTS_N 1216
 #endif
@@ -185,6 +137,8 @@ struct AclStage {
     // its list found as in issue()
     // returns true when an entry flag of the round is not 1 (checked only
     // with chk: the walk speculated that every entry is present)
+    // (an entry is five aligned dword LDS reads and four v_alignbyte: 1M Small
+    // 0.760 -> 0.747 ms against two 16-byte reads and window16's select chain)
     template <class AfterWait>
     HONU_DEV bool store(const uint8_t *ws, honu_acl *__restrict__ acl, uint64_t ao, bool ok,
                         bool chk, AfterWait after_wait) const {
@@ -223,9 +177,6 @@ struct AclStage {
             const uint32_t q = rl + 18 * j + 1;
             uint64_t lo, hi;
             uint32_t pm;
-#if FILL_DW
-            // five aligned dwords and four v_alignbyte instead of two 16-byte
-            // reads and the per-lane select chain of window16
             const uint32_t sh = q & 3u;
             const __attribute__((address_space(3))) uint32_t *w =
                 (const __attribute__((address_space(3))) uint32_t *)(ws + (q & ~3u));
@@ -233,14 +184,6 @@ struct AclStage {
             lo = ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32) | __builtin_amdgcn_alignbyte(d1, d0, sh);
             hi = ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, sh) << 32) | __builtin_amdgcn_alignbyte(d3, d2, sh);
             pm = (d4 >> (8 * sh)) & 0xFF;
-#else
-            const uint32_t qa = q & ~15u, sft = q & 15u;
-            const u32x4 a = *reinterpret_cast<const u32x4 *>(ws + qa);
-            const u32x4 b = *reinterpret_cast<const u32x4 *>(ws + qa + 16);
-            window16(a, b, sft, lo, hi);
-            const uint32_t bw = (sft >> 2) == 0 ? b.x : (sft >> 2) == 1 ? b.y : (sft >> 2) == 2 ? b.z : b.w;
-            pm = (bw >> (8 * (sft & 3))) & 0xFF;
-#endif
             if (chk && e < etot)
                 bad |= ((const __attribute__((address_space(3))) uint8_t *)ws)[q - 1] != 1;
             if (e < etot && rt != ~0ull) {
@@ -301,21 +244,23 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     const uint64_t ntiles = (n + HONU_WAVE - 1) / HONU_WAVE;
     const uint64_t waves = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
     // every tile has a resident wave of its own: static tiles (lookback.h)
-    const bool stat = ntiles <= waves && !(O.dbg & 4);
     // (measured: taking the next ticket and loading its bounds before the
     // look-back wait, to overlap them with it, doubled the wait: tiles are
     // then handed out ~40 us before their waves start them, which spreads the
     // publish times of consecutive tiles)
-    const bool stat_idx = stat || FUSED_STATIC_ALL || (O.dbg & 4);  // dbg 4: measurement only (with 2), static tiles at any size
+    const bool stat_idx = ntiles <= waves;
     uint64_t k_static = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + threadIdx.x / HONU_WAVE;
     WSTAMP_START();
     // ticket mode: the next tile's ticket is requested once the current tile's
     // last ACL staging round has landed (its table stores and the rest of the
-    // tile then hide the atomic's round trip), or at the tile's end when it
-    // staged nothing (FUSED_EARLY_TICKET)
+    // tile then hide the atomic's round trip: -0.8 %), or at the tile's end
+    // when it staged nothing. A workgroup takes the first tiles of its waves
+    // with one atomic (4 tickets), so a launch starts with 512 ticket atomics
+    // on the one address instead of 2,048 (1M Small 0.780 -> 0.757 ms, 262 K
+    // Large 0.258 -> 0.238 ms, profiles/r03/ab/wg_ticket_ab.jsonl).
     uint32_t tk = 0;
     bool tk_pending = false;
-    if (FUSED_WG_TICKET && !stat_idx) {  // wave-uniform, and the same in every wave of the workgroup
+    if (!stat_idx) {  // wave-uniform, and the same in every wave of the workgroup
         if (threadIdx.x == 0)
             wg_ticket = __hip_atomic_fetch_add(&lb->ticket, (uint32_t)HONU_WAVES_PER_BLOCK, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT);
@@ -323,8 +268,6 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         tk = wg_ticket + threadIdx.x / HONU_WAVE;
         tk_pending = true;
     }
-    TileHead Hn;  // FUSED_PREFETCH: the next static tile's head
-    bool have_next = false;
     for (;;) {
         uint64_t t;
         if (stat_idx) {
@@ -340,22 +283,13 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         const uint64_t i0 = t * HONU_WAVE, i = i0 + lane;
         const bool valid = i < n;
         TileHead H;
-        if (FUSED_PREFETCH && have_next) {
-            H = Hn;
-        } else {
-            tile_head_bounds(i0, rec_off, n, H);
-            tile_head_bytes(rec, H);
-        }
+        tile_head_bounds(i0, rec_off, n, H);
+        tile_head_bytes(rec, H);
         WinParse P;
-#if FUSED_MEMROW
-        MemRow R;
-        R.p = valid ? reinterpret_cast<uint8_t *>(O.meta + i) : nullptr;
-#else
         RegRow R;
-#endif
         SpecPub early;
-        early.on = mode == 1 && !(O.dbg & 2);
-        early.spec_acl = early.on && FUSED_SPEC_ACL;
+        early.on = mode == 1;
+        early.spec_acl = early.on;
         early.status = lb_status;
         early.t = t;
         early.ep = ep;
@@ -379,28 +313,18 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
             x2 = wave_excl(c2, agg[2]);
             // publish, then write the rows while the predecessors finish
             // (their list offsets are patched in below)
-            if (!(O.dbg & 2)) lb_publish<3>(lb_status, t, ep, agg);
+            lb_publish<3>(lb_status, t, ep, agg);
         }
-#if !FUSED_MEMROW
         rows_out(ws, R, i0, n, O.meta);
-#endif
-        const bool pf = FUSED_PREFETCH && stat_idx && k_static < ntiles;  // wave-uniform
-        have_next = pf;
-        if (pf) tile_head_bounds(k_static * HONU_WAVE, rec_off, n, Hn);
         // the ACL lists with every entry present go to the table from LDS: the
         // first round of their blocks is staged now, before the wait, as it
         // needs no offsets
         const bool fl = valid && P.st == HONU_OK && P.nacl && (P.acl_pos & GRP_ACL_FAST);
         AclStage S;
         S.init(fl, P.acl_pos & GRP_POS_MASK, P.nacl);
-        if (S.more() && !(O.dbg & 1)) S.issue(ws, rec);
+        if (S.more()) S.issue(ws, rec);
         WSTAMP(10);  // publish + rows out + first staging round issued
-        if (O.dbg & 2) {
-            excl[0] = excl[1] = excl[2] = 0;
-        } else {
-            lb_resolve<3>(lb_status, t, ep, agg, excl);
-        }
-        if (pf) tile_head_bytes(rec, Hn);
+        lb_resolve<3>(lb_status, t, ep, agg, excl);
         WSTAMP(11);  // look-back wait
         if (t == ntiles - 1 && lane < 3)
             O.totals[lane] = lane == 0 ? excl[0] + agg[0] : (lane == 1 ? excl[1] + agg[1] : excl[2] + agg[2]);
@@ -473,23 +397,33 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
                     p += 1;
                 }
             }
+        } else if (early.spec_acl && valid && P.st == HONU_OK && P.nacl && (P.acl_pos & GRP_ACL_FAST) &&
+                   !S.staged()) {
+            // the record failed the capacity check, so nothing is stored, but
+            // its speculated list's flags still decide whether the walk read
+            // the fields after the list at the right place (staged lists are
+            // checked by S.store whatever the capacity verdict)
+            for (uint64_t k = 0; k < P.nacl; k++)
+                if (rec[apos + 18 * k] != 1) {
+                    acl_bad = true;
+                    break;
+                }
         }
         WSTAMP(12);  // info, regions, lists with nil entries
         // staged lists: round by round, lane e of a pass takes entry e of the
         // round's entries (one run of the table per record), reads its 17
         // bytes from LDS and stores the 20-byte row
-        if (!(O.dbg & 1))
-            while (S.more()) {
-                const bool last = S.stop >= S.nbtot;  // wave-uniform
-                acl_bad |= S.store(ws, O.acl, ao, ok, early.spec_acl, [&]() {
-                    if (FUSED_EARLY_TICKET && last && !stat_idx) {
-                        tk = lb_ticket_issue(lb);
-                        tk_pending = true;
-                    }
-                });
-                S.advance();
-                if (S.more()) S.issue(ws, rec);
-            }
+        while (S.more()) {
+            const bool last = S.stop >= S.nbtot;  // wave-uniform
+            acl_bad |= S.store(ws, O.acl, ao, ok, early.spec_acl, [&]() {
+                if (last && !stat_idx) {
+                    tk = lb_ticket_issue(lb);
+                    tk_pending = true;
+                }
+            });
+            S.advance();
+            if (S.more()) S.issue(ws, rec);
+        }
         // a speculated list had an entry that is not present (nil, or a bad
         // flag): the walk read the fields after it at the wrong place. A
         // record that failed after a speculated list is not filled, so its
@@ -527,17 +461,12 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
     const uint64_t tiles = (n + HONU_WAVE - 1) / HONU_WAVE;
     uint64_t b = (tiles + HONU_WAVES_PER_BLOCK - 1) / HONU_WAVES_PER_BLOCK;
     if (max_blocks > 0 && b > (uint64_t)max_blocks) b = (uint64_t)max_blocks;
-#ifdef HONU_AB  // measurement knobs, A/B library only (they break the results)
-    static const int dbg = getenv("HONU_FUSED_DBG") ? atoi(getenv("HONU_FUSED_DBG")) : 0;
-#else
-    const int dbg = 0;
-#endif
-    DecodeOut O{meta, info, acl, acl_cap, reg, reg_cap, data_cap, materialize, scratch, offs, totals, dbg};
+    DecodeOut O{meta, info, acl, acl_cap, reg, reg_cap, data_cap, materialize, scratch, offs, totals};
     // speculation pays where tiles queue for tickets (1M Small 0.866 -> 0.840
     // ms with the publish alone, -> 0.778 with the ACL flags too) and, since
     // the flag gather is gone, in static-tile launches of ~1000 tiles and more
     // (profiles/r03/fused_spec_ab.jsonl, spec_acl_ab*.jsonl)
-    if (!FUSED_SPEC || tiles < FUSED_SPEC_MIN_TILES) {
+    if (tiles < FUSED_SPEC_MIN_TILES) {
         hipLaunchKernelGGL(k_decode_fused<0>, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off,
                            n, O, lb, lb_status, lb_words);
         return hipGetLastError();

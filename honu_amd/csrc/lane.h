@@ -216,6 +216,11 @@ HONU_DEV uint32_t uvarint_bytes(uint64_t x, uint64_t &lo, uint64_t &hi) {
 // places with most lanes active, instead of from every put() with the few
 // lanes whose chunk just filled (42 % fewer store instructions; the encoder
 // is bound by the L1's miss queue, so this bought 1 %: DESIGN §3).
+// ENC_ABL (measurement only, wrong output): 1 frame bodies not loaded, 2 ACL
+// end entries not loaded, 4 regions not loaded, 8 no chunk stores
+#ifndef ENC_ABL
+#define ENC_ABL 0
+#endif
 template <int R>
 struct LaneWriterT {
     uint8_t *out;
@@ -226,7 +231,7 @@ struct LaneWriterT {
     uint64_t hpos;    // parked head chunk (hfirst != 0): offset, first byte, bytes
     uint32_t hfirst;
     uint64_t h0, h1;
-    u32x4 *ring;      // R > 0: this lane's slot 0 (slot k at ring[k * HONU_BLOCK])
+    u32x4 *ring;      // R > 0: this lane's slot 0 (slot k at ring[k * HONU_WAVE]: per-wave rings)
     uint32_t nch;     // R > 0: full chunks in the ring, ending just before cpos
 
     HONU_DEV void init(uint8_t *o, uint64_t pos) {
@@ -258,9 +263,9 @@ struct LaneWriterT {
         if (first == 0) {
             const u32x4 v{(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32)};
             if constexpr (R > 0) {
-                ring[((cpos >> 4) & (R - 1)) * HONU_BLOCK] = v;
+                ring[((cpos >> 4) & (R - 1)) * HONU_WAVE] = v;
                 nch++;
-            } else {
+            } else if (!(ENC_ABL & 8)) {
                 *reinterpret_cast<u32x4 *>(out + cpos) = v;
             }
         } else {  // the head chunk: parked until finish()
@@ -319,7 +324,7 @@ struct LaneWriterT {
 #pragma unroll
             for (int j = 0; j < 5; j++) {
                 u32x4 v{0, 0, 0, 0};
-                if (q0 + j < nw) v = w[q0 + j];
+                if (!(ENC_ABL & 1) && q0 + j < nw) v = w[q0 + j];
                 x[2 * j] = ((uint64_t)v.y << 32) | v.x;
                 x[2 * j + 1] = ((uint64_t)v.w << 32) | v.z;
             }
@@ -345,8 +350,8 @@ struct LaneWriterT {
     HONU_DEV void drain() {
         if constexpr (R > 0) {
             const uint64_t p0 = cpos - 16ull * nch;
-            for (uint32_t k = 0; k < nch; k++)
-                *reinterpret_cast<u32x4 *>(out + p0 + 16 * k) = ring[(((p0 >> 4) + k) & (R - 1)) * HONU_BLOCK];
+            for (uint32_t k = 0; k < nch && !(ENC_ABL & 8); k++)
+                *reinterpret_cast<u32x4 *>(out + p0 + 16 * k) = ring[(((p0 >> 4) + k) & (R - 1)) * HONU_WAVE];
             nch = 0;
         }
     }
@@ -440,7 +445,7 @@ HONU_DEV uint64_t encode_tail_bytes_noacl(const honu_meta &m, const uint32_t *__
     for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
         uint32_t r8[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? reg[ro + k0 + j] : 0;
+        for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? ((ENC_ABL & 4) ? 1000u * j : reg[ro + k0 + j]) : 0;
 #pragma unroll
         for (int j = 0; j < 8; j++) t += k0 + j < nr ? uvarint_len(r8[j]) : 0;
     }
@@ -535,7 +540,7 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
         for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
             uint32_t r8[8];
 #pragma unroll
-            for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? reg[ro + k0 + j] : 0;
+            for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? ((ENC_ABL & 4) ? 1000u * j : reg[ro + k0 + j]) : 0;
 #pragma unroll
             for (int j = 0; j < 8; j++) sfx += k0 + j < nr ? uvarint_len(r8[j]) : 0;
         }
@@ -554,8 +559,8 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
             const uint64_t T = (E & ~15ull) > hend ? (E & ~15ull) : hend;
             // the list's encoding at both ends (acl_chunk: 16 bytes from the
             // <= 2 entries they straddle), both loaded at once
-            const u32x4 hv = acl_chunk(acl + ao, na, P, P);
-            const u32x4 tv = E > T ? acl_chunk(acl + ao, na, P, T) : u32x4{0, 0, 0, 0};
+            const u32x4 hv = (ENC_ABL & 2) ? u32x4{1, 2, 3, 4} : acl_chunk(acl + ao, na, P, P);
+            const u32x4 tv = (ENC_ABL & 2) ? u32x4{5, 6, 7, 8} : E > T ? acl_chunk(acl + ao, na, P, T) : u32x4{0, 0, 0, 0};
             auto put_n = [&](const u32x4 &v, uint32_t cnt) {  // the first cnt (< 16) bytes of v
                 const uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
                 if (cnt >= 8) {
@@ -602,7 +607,7 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
     for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
         uint32_t r8[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? reg[ro + k0 + j] : 0;
+        for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? ((ENC_ABL & 4) ? 1000u * j : reg[ro + k0 + j]) : 0;
         W.drain();  // <= 15 + 10 before the first batch, <= 40 after one
 #pragma unroll
         for (int j = 0; j < 8; j++)

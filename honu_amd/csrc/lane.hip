@@ -16,31 +16,84 @@ namespace honu {
 #define ENC_RING 8  // chunks in the writer's LDS ring per lane (0: direct stores)
 #endif
 
+// ENC_ROWS_LDS: the wave's 64 rows (contiguous, 22.5 KB) reach the lanes
+// through LDS: two passes of 32 rows, each 11 coalesced 1 KB global_load_lds
+// instructions, then every lane of the pass reads its row from LDS. Loaded
+// per lane, each of a row's 22 16-byte loads touches 64 cache lines (one per
+// record); the L1's per-line load path is what bounds this kernel.
+#ifndef ENC_ROWS_LDS
+#define ENC_ROWS_LDS 0
+#endif
+#ifndef ENC_ROW_PASS_N
+#define ENC_ROW_PASS_N 32
+#endif
+constexpr uint32_t ENC_ROW_PASS = ENC_ROW_PASS_N;                                   // rows per staging pass
+constexpr uint32_t ENC_ROW_BYTES = ENC_ROW_PASS * sizeof(honu_meta);     // 11,264 = 11 x 1 KB
+constexpr uint32_t ENC_RING_BYTES = (ENC_RING > 0 ? ENC_RING : 1) * HONU_WAVE * 16;
+constexpr uint32_t ENC_WAVE_BYTES = ENC_ROWS_LDS && ENC_ROW_BYTES > ENC_RING_BYTES ? ENC_ROW_BYTES : ENC_RING_BYTES;
+static_assert(ENC_ROW_BYTES % 1024 == 0, "whole DMA instructions");
+
 template <bool SKIP_ACL>
-HONU_DEV void k_encode_meta_lane_one(uint64_t i, const honu_meta *__restrict__ meta, const uint8_t *__restrict__ var,
+HONU_DEV void k_encode_meta_lane_one(uint64_t i, const honu_meta &m, const uint8_t *__restrict__ var,
     const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
-    const uint64_t *__restrict__ payload_off, uint64_t n, uint8_t *__restrict__ out,
+    const uint64_t *__restrict__ payload_off, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status,
     uint64_t *__restrict__ acl_out, u32x4 *ring) {
-    ESTAMP(0);  // entered
     if (status[i] != HONU_OK) return;
     const uint64_t beg = out_off[i], end = out_off[i + 1];
     if (end > out_cap) {
         status[i] = HONU_ERR_CAPACITY;
         return;
     }
-    // the whole row in registers first (loads cannot pass the output stores)
-    honu_meta m;
-    {
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(meta + i);
-        u32x4 *dstr = reinterpret_cast<u32x4 *>(&m);
-#pragma unroll
-        for (int k = 0; k < 22; k++) dstr[k] = src[k];
-    }
     const uint64_t dlen = payload_off[i + 1] - payload_off[i];
     const uint64_t pos = encode_record_lane<SKIP_ACL, SKIP_ACL ? ENC_RING : 0>(m, var, acl, reg, dlen, beg, end,
                                                                            out, ring);
     if constexpr (SKIP_ACL) acl_out[i] = pos;
+}
+
+// a lane's row straight from global memory (the loads cannot pass the output
+// stores, so the whole row is loaded first)
+HONU_DEV void load_row(const honu_meta *__restrict__ src, honu_meta &m) {
+    const u32x4 *s = reinterpret_cast<const u32x4 *>(src);
+    u32x4 *d = reinterpret_cast<u32x4 *>(&m);
+#pragma unroll
+    for (int k = 0; k < 22; k++) d[k] = s[k];
+}
+
+// rows [t0, t0 + 64) of meta (clipped to n) into this lane's m, through the
+// wave's LDS area (ENC_ROW_BYTES): wave-uniform call
+HONU_DEV void stage_rows(uint8_t *area, const honu_meta *__restrict__ meta, uint64_t t0, uint64_t n,
+                         honu_meta &m) {
+    const uint32_t lane = lane_id();
+    const uint8_t *src = reinterpret_cast<const uint8_t *>(meta + t0);
+#pragma unroll 1
+    for (uint32_t h = 0; h < HONU_WAVE / ENC_ROW_PASS; h++) {
+        const uint64_t r0 = t0 + h * ENC_ROW_PASS;
+        const uint64_t rows = r0 >= n ? 0 : (n - r0 < ENC_ROW_PASS ? n - r0 : ENC_ROW_PASS);
+        if (!rows) break;  // wave-uniform
+        const uint32_t bytes = (uint32_t)rows * (uint32_t)sizeof(honu_meta);
+        wave_sync();  // the area's previous reads (ring drains, pass h - 1) are done
+#pragma unroll
+        for (uint32_t k = 0; k < ENC_ROW_BYTES / 1024; k++)
+            if (1024 * k + 16 * lane < bytes)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(src + h * ENC_ROW_BYTES + 1024 * k + 16 * lane),
+                    (__attribute__((address_space(3))) void *)(area + 1024 * k), 16, 0, 0);
+        __builtin_amdgcn_s_waitcnt(0);
+        wave_sync();
+        // every lane reads (its own row in its pass), then keeps what is its
+        // own by a per-dword select: no branch, so the row lives in one set
+        // of registers (a branch per pass kept two copies: 246 VGPRs)
+        const bool mine = lane / ENC_ROW_PASS == h;
+        const u32x4 *s = reinterpret_cast<const u32x4 *>(area + (lane % ENC_ROW_PASS) * sizeof(honu_meta));
+        u32x4 *d = reinterpret_cast<u32x4 *>(&m);
+#pragma unroll
+        for (int k = 0; k < 22; k++) {
+            const u32x4 v = s[k];
+            d[k] = u32x4{mine ? v.x : d[k].x, mine ? v.y : d[k].y, mine ? v.z : d[k].z, mine ? v.w : d[k].w};
+        }
+    }
+    wave_sync();  // the area becomes the writer's ring
 }
 
 template <bool SKIP_ACL>
@@ -50,11 +103,26 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
     const uint64_t *__restrict__ payload_off, uint64_t n, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status,
     uint64_t *__restrict__ acl_out) {
-    __shared__ u32x4 ring[(ENC_RING > 0 ? ENC_RING : 1) * HONU_BLOCK];  // slot-major, lanes adjacent
-    for (uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * HONU_BLOCK)
-        k_encode_meta_lane_one<SKIP_ACL>(i, meta, var, acl, reg, payload_off, n, out, out_cap, out_off, status,
-                                         acl_out, ring + threadIdx.x);
+    // per wave: the writer's ring (slot-major, lanes adjacent), and with
+    // ENC_ROWS_LDS first the row staging
+    __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * ENC_WAVE_BYTES];
+    uint8_t *area = smem + (threadIdx.x / HONU_WAVE) * ENC_WAVE_BYTES;
+    u32x4 *ring = reinterpret_cast<u32x4 *>(area) + lane_id();
+    // wave-uniform loop over tiles of 64 records (one per lane)
+    for (uint64_t t0 = (uint64_t)blockIdx.x * HONU_BLOCK + (threadIdx.x & ~(uint64_t)(HONU_WAVE - 1)); t0 < n;
+         t0 += (uint64_t)gridDim.x * HONU_BLOCK) {
+        const uint64_t i = t0 + lane_id();
+        ESTAMP(0);  // entered
+        honu_meta m;
+#if ENC_ROWS_LDS
+        stage_rows(area, meta, t0, n, m);
+#else
+        if (i < n) load_row(meta + i, m);
+#endif
+        if (i < n)
+            k_encode_meta_lane_one<SKIP_ACL>(i, m, var, acl, reg, payload_off, out, out_cap, out_off, status,
+                                             acl_out, ring);
+    }
 }
 
 #undef OFF

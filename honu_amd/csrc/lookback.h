@@ -12,8 +12,11 @@
 // Status word: bits 63:62 flag (0 none, 1 aggregate, 2 inclusive), 61:44 the
 // launch epoch (18 bits), 43:0 the value (< 2^44: the counts are bounded by the
 // bytes of one arena). Words of earlier launches carry another epoch, so the
-// array is never cleared between launches; the last wave of a launch resets
-// the ticket, advances the epoch and, when the epoch wraps, clears the array.
+// array is never cleared between launches; the end of a launch resets the
+// ticket, advances the epoch and, when the epoch wraps, clears the array:
+// lb_finish_blocks (the last workgroup to finish) ends every single-launch
+// decode (fused.hip, static tiles and tickets alike); lb_finish (the wave
+// holding the last ticket) ends the scans (scan.hip).
 // Launch at most as many waves as fit the chip at once: every ticket is one
 // atomic on one address, so tickets should be few per wave, not per tile.
 // Nothing is passed from the host per launch, so the kernels replay from a
@@ -138,6 +141,7 @@ HONU_DEV void lb_resolve(uint64_t *status, uint64_t t, uint32_t ep, const uint64
         if (lane == (uint32_t)c) lb_store(status + t * K + c, lb_word(2, ep, excl[c] + agg[c]));
 }
 
+// The scans' end (scan.hip; the single-launch decode ends in lb_finish_blocks).
 // Called by every wave with the ticket that ended its loop (t_end >= ntiles):
 // a wave takes that ticket only after finishing its last tile, so the wave
 // holding ticket ntiles + waves - 1 is the last one of the launch. It resets

@@ -28,14 +28,12 @@ namespace honu {
 
 #define GO_MAX_ALLOC (1ull << 48)  // runtime maxAlloc, linux/amd64
 
-// WIN_MIRROR: the pad slot of every window holds a copy of ring slot 0, so a
-// 16-byte field read is five aligned dword reads with no wrap and four
-// v_alignbyte, not two 16-byte reads and a per-lane select chain (1M Small
-// zero copy 0.751 -> 0.736 ms, 262 K Large 239 -> 234 us, split parse of 16 K
-// Small 63.2 -> 61.8 us; profiles/r03/ab/win_mirror_ab.jsonl)
-#ifndef WIN_MIRROR
-#define WIN_MIRROR 1
-#endif
+// The pad slot of every window (slot 16, there for bank spreading) holds a
+// copy of ring slot 0, so a 16-byte field read is five aligned dword reads
+// with no wrap and four v_alignbyte, not two 16-byte reads and a per-lane
+// select chain (1M Small zero copy 0.751 -> 0.736 ms, 262 K Large 239 -> 234
+// us, split parse of 16 K Small 63.2 -> 61.8 us;
+// profiles/r03/ab/win_mirror_ab.jsonl)
 constexpr uint32_t WB = 256;           // window bytes per lane (16 blocks)
 constexpr uint32_t WSL = WB / 16 + 1;  // LDS stride in 16-byte slots: one pad slot per
                                        // window puts the lanes of a ds_read_b128 group
@@ -82,15 +80,9 @@ struct LaneWin {
             const uint32_t s = 64 * k + lane;
             const uint32_t L = s / WSL, c = s % WSL;
             const uint64_t b = wants[L];
-#if WIN_MIRROR
             if (b != NOWIN) {  // slot 16 mirrors ring slot 0 (fetch16 reads across the wrap)
                 const uint64_t w0 = b >> 4;
                 const uint64_t blk = w0 + (((c & 15) - w0) & 15);  // the block of [w0, w0+16) in slot c
-#else
-            if (c < WB / 16 && b != NOWIN) {
-                const uint64_t w0 = b >> 4;
-                const uint64_t blk = w0 + ((c - w0) & 15);  // the block of [w0, w0+16) in slot c
-#endif
                 const uint64_t o = olds[L];
                 const bool held = o != NOWIN && blk >= (o >> 4) && blk < (o >> 4) + 16;
                 if (!held && 16 * blk < lims[L])
@@ -115,7 +107,6 @@ struct LaneWin {
         return ((const __attribute__((address_space(1))) uint8_t *)rec)[p];
     }
     HONU_DEV void fetch16(uint64_t p, uint64_t end, uint64_t &lo, uint64_t &hi) const {
-#if WIN_MIRROR
         if (wb != NOWIN && p >= wb && p - wb <= WB - 16) {
             // [p, p + 16) as five aligned dwords of the lane's slots (slot 16
             // mirrors slot 0, so the run never wraps) and four v_alignbyte
@@ -129,16 +120,6 @@ struct LaneWin {
             return;
         }
         lane_fetch16(rec, p, end, lo, hi);
-#else
-        if (wb != NOWIN && p >= wb && p - wb <= WB - 16) {
-            const uint64_t blk = p >> 4;
-            const u32x4 a = *reinterpret_cast<const u32x4 *>(slot(blk));
-            const u32x4 b = *reinterpret_cast<const u32x4 *>(slot(blk + 1));
-            window16(a, b, (uint32_t)(p & 15), lo, hi);
-        } else {
-            lane_fetch16(rec, p, end, lo, hi);
-        }
-#endif
     }
 };
 
@@ -253,12 +234,11 @@ static __device__ uint64_t g_stage_last[1 << 16];
     } while (0)
 #endif
 
-// Where the walk puts the decoded row (metadata.go:202-302 field by field).
-// RegRow: the whole 352-byte row in 88 registers, out in one coalesced pass
-// afterwards (rows_out). MemRow: every field stored to the lane's row as it is
-// decoded, the fields of absent sub-structs zeroed when their nil flag is
-// read, the whole row zeroed when the walk fails (Go returns nil, err) or the
-// Metadata is nil (object.go:76-82) — 88 registers fewer, scattered stores.
+// Where the walk puts the decoded row (metadata.go:202-302 field by field):
+// the whole 352-byte row in 88 registers, out in one coalesced pass afterwards
+// (rows_out). (Rows stored field by field as they are decoded free the
+// registers but were 30 % slower: vmcnt counts stores, so every window refill
+// waited for them; DESIGN §3, source in git history at 88edda1.)
 struct RegRow : Row {
     HONU_DEV void begin() { clear(); }
     template <int OFF, int LEN> HONU_DEV void zero() {}  // begin() cleared it
@@ -266,60 +246,6 @@ struct RegRow : Row {
         (void)hm;
         u32((int)offsetof(honu_meta, present), pr);
         if (!st_ok) clear();
-    }
-};
-struct MemRow {
-    uint8_t *p;      // this lane's row, nullptr past n
-    uint32_t b0, b1;  // row bytes 4..11 (permissions .. signature_alg, pad)
-
-    HONU_DEV void begin() { b0 = b1 = 0; }
-    HONU_DEV void s32(int off, uint32_t v) {
-        if (p) *reinterpret_cast<uint32_t *>(p + off) = v;
-    }
-    HONU_DEV void s64(int off, uint64_t v) {
-        if (p) *reinterpret_cast<uint64_t *>(p + off) = v;
-    }
-    HONU_DEV void s128(int off, uint64_t lo, uint64_t hi) {
-        if (p)
-            *reinterpret_cast<u32x4 *>(p + off) =
-                u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-    }
-    HONU_DEV void u8(int off, uint32_t v) {  // bytes 4..10, stored by finish()
-        if (off < 8) b0 |= (v & 0xFF) << (8 * (off - 4));
-        else b1 |= (v & 0xFF) << (8 * (off - 8));
-    }
-    HONU_DEV void u32(int off, uint32_t v) { s32(off, v); }
-    HONU_DEV void u64(int off, uint64_t v) { s64(off, v); }
-    HONU_DEV void bytes16(int off, uint64_t lo, uint64_t hi) { s128(off, lo, hi); }
-    HONU_DEV void span(int off, uint64_t o, uint64_t l) { s128(off, o, l); }
-    // zeros over [OFF, OFF + LEN) (compile-time, 4-aligned), widest stores first
-    template <int OFF, int LEN> HONU_DEV void zero() {
-        static_assert(OFF % 4 == 0 && LEN % 4 == 0, "dword granularity");
-        if constexpr (LEN > 0) {
-            if constexpr (OFF % 16 == 0 && LEN >= 16) {
-                s128(OFF, 0, 0);
-                zero<OFF + 16, LEN - 16>();
-            } else if constexpr (OFF % 8 == 0 && LEN >= 8) {
-                s64(OFF, 0);
-                zero<OFF + 8, LEN - 8>();
-            } else {
-                s32(OFF, 0);
-                zero<OFF + 4, LEN - 4>();
-            }
-        }
-    }
-    HONU_DEV void finish(bool st_ok, bool hm, uint32_t pr) {
-        if (!(st_ok && hm)) {  // every byte zero (present too)
-            zero<0, (int)sizeof(honu_meta)>();
-            return;
-        }
-        s32(0, pr);
-        s32(4, b0);
-        s32(8, b1);
-        s32(60, 0);                                   // padding
-        s64(88, 0);
-        s64((int)offsetof(honu_meta, acl_off), 0);    // set after the offsets scan
-        s64((int)offsetof(honu_meta, regions_off), 0);
     }
 };
 
@@ -381,7 +307,7 @@ HONU_DEV void tile_head_bytes(const uint8_t *__restrict__ rec, TileHead &H) {
 // of record i0 + lane, the lani walk of metadata.go:202-302. Wave-uniform
 // call (every lane of the wave, i0 the same): the window refills need the
 // whole wave. H: the tile's bounds and header bytes (tile_head_*). The row
-// goes to R (RegRow / MemRow, acl_off / regions_off not yet set).
+// goes to R (RegRow, acl_off / regions_off not yet set).
 template <class RowT, class EarlyT>
 HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restrict__ rec,
                        uint64_t n, const TileHead &H, RowT &R, WinParse &P, EarlyT &early) {

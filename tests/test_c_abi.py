@@ -32,3 +32,30 @@ def test_c_demo_marshal_decode(shape, n):
     r = subprocess.run([DEMO, str(shape), str(n)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert r.stdout.startswith("ok:")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,n", [(2, 512), (0, 20000)], ids=["large", "small"])
+def test_c_demo_count_sized_tables_vs_oracle(tmp_path, oracle_lib, shape, n):
+    """The binding's DecodeBatch flow: ACL / region tables
+    sized by the batch's entry counts through the retry on the totals the
+    first call reports (its caps are one entry per record, so the retry always
+    runs), not by record bytes. Everything the zero-copy decode returned is
+    bit-exact with the oracle's decode of the same records, and the tables
+    take their exact entry counts: a small fraction of the records arena."""
+    import numpy as np
+    from honu_amd.metadata import ACL_DTYPE, INFO_DTYPE, META_DTYPE
+    r = subprocess.run([DEMO, str(shape), str(n), str(tmp_path)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "decode calls 2," in r.stdout
+    rd = lambda name, dt: np.fromfile(tmp_path / name, dtype=dt)  # noqa: E731
+    rec, off = rd("rec.bin", np.uint8), rd("off.bin", np.uint64)
+    ometa, oinfo, oacl, oreg, _, otot = oracle_lib.decode_batch(rec, off, False)
+    assert np.array_equal(rd("tot.bin", np.uint64), otot)
+    assert rd("meta.bin", META_DTYPE).tobytes() == ometa.tobytes()
+    assert rd("info.bin", INFO_DTYPE).tobytes() == oinfo.tobytes()
+    assert rd("acl.bin", ACL_DTYPE).tobytes() == oacl.tobytes()
+    assert rd("reg.bin", np.uint32).tobytes() == oreg.tobytes()
+    table_bytes = 20 * int(otot[0]) + 4 * int(otot[1])
+    assert f"table bytes {table_bytes} " in r.stdout
+    assert table_bytes < 0.5 * len(rec)  # byte-sized tables would be 24x the arena

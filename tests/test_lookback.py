@@ -8,9 +8,13 @@ word of the first one is taken for its own. Also: batches of 1..300 tiles in
 a row, each checked against the oracle (every look-back window size).
 
 Launches whose tiles all fit the resident waves take static tiles (one per
-wave, no ticket atomics, lookback.h lb_finish_blocks); larger ones take
-tickets (lb_finish). Both advance the same epoch: the last test alternates
-them, across an epoch wrap reached by static launches."""
+wave, no ticket atomics); larger ones take tickets. Every single-launch decode
+ends in lookback.h lb_finish_blocks (a per-workgroup done count whose last
+arrival advances the epoch, resets the ticket and clears misspec; lb_finish is
+the scans' form). Both tile modes advance the same epoch: a test alternates
+them, across an epoch wrap reached by static launches. Then the speculative
+launches' recovery (late-failing records, nil ACL entries, a long unstaged list
+under a capacity failure) and concurrent launches on two streams."""
 import numpy as np
 import pytest
 
@@ -267,3 +271,52 @@ def test_concurrent_ticket_and_static_launches_on_two_streams(oracle_lib):
     finally:
         c1.close()
         c2.close()
+
+
+def test_speculated_long_list_checked_under_capacity_failure(oracle_lib):
+    """A speculated ACL list too long to be staged (1,200 entries: more than
+    STAGE_SLOTS blocks) whose last entry is nil, in the last record of a
+    2188-tile batch, with acl_cap one entry short of the batch's total so that
+    this record fails the capacity check. Its suffix is crafted so that the
+    walk, which took the list as all present (17 bytes too long), still parses
+    the bytes after it (as 0 regions instead of 5): only the entry flags reveal
+    the misspeculation. They must be checked although the record stores
+    nothing, and the guarded launch then redoes the batch:
+    totals, rows, info (CAPACITY for that record) and the tables equal the
+    oracle's with the same caps."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from honu_amd.metadata import AccessControl, Metadata, pack_batch
+    n = 140000
+    rec, off, _ = oracle_lib.marshal_batch(gen_host_batch(45, "small", 0, n - 1))
+    acl = [AccessControl(bytes([(7 * j + k) & 0xFF for k in range(16)]), j & 0xFF) for j in range(1199)]
+    m = Metadata(ObjectID=bytes(range(16)), MIME="x", ACL=acl + [None],
+                 WriteRegions=[(1 << 21) + 1, 1 << 22, 1 << 23, 1 << 24, 0])
+    r2, o2, st2 = oracle_lib.marshal_batch(pack_batch([m], [b"payload"]))
+    assert (st2 == 0).all()
+    assert r2[-7:].tobytes() == bytes(7)  # last region 0, then six zero bytes
+    brec = np.concatenate([rec, r2])
+    boff = np.concatenate([off, off[-1] + o2[1:]]).astype(np.uint64)
+    ometa, oinfo, oacl, oreg, _, otot = oracle_lib.decode_batch(brec, boff, False)
+    assert int(ometa[-1]["regions_count"]) == 5 and int(ometa[-1]["acl_count"]) == 1200
+    acl_cap, reg_cap = int(otot[0]) - 1, int(otot[1]) + 16
+    c = hobj.Codec(0, n)
+    try:
+        hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
+        d = _Dec(c, brec, boff)
+        d.acl_cap, d.reg_cap = acl_cap, reg_cap
+        assert d() == 0
+        torch.cuda.synchronize()
+        tot = d.tot[:24].cpu().numpy().view(np.uint64)
+        assert np.array_equal(tot, otot)
+        assert d.meta[:352 * n].cpu().numpy().tobytes() == ometa.tobytes()
+        info = np.frombuffer(d.info[:32 * n].cpu().numpy().tobytes(), oinfo.dtype)
+        want = oinfo.copy()
+        want["meta_status"][-1] = 9  # HONU_ERR_CAPACITY
+        assert info.tobytes() == want.tobytes()
+        nacl = int(otot[0]) - 1200  # the entries of every record before the last
+        assert d.acl[:20 * nacl].cpu().numpy().tobytes() == oacl[:nacl].tobytes()
+        nreg = int(otot[1]) - 5  # the capacity-failed record stores no regions either
+        assert d.reg[:4 * nreg].cpu().numpy().tobytes() == oreg[:nreg].tobytes()
+    finally:
+        c.close()
