@@ -609,8 +609,8 @@ class DecodeBench:
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": gbs / HBM_PEAK_GBS,
-                "traffic": (pmc_traffic(self.workload("zero_copy"), "k_decode_fused<1>")
-                            or pmc_traffic(self.workload("zero_copy"), "k_decode_fused<0>")),
+                "traffic": (pmc_traffic(self.workload("zero_copy"), "k_decode_fused<1")
+                            or pmc_traffic(self.workload("zero_copy"), "k_decode_fused<0")),
                 "avg_launch_ms": t * 1e3,
                 "algorithmic_bytes_per_launch": self.meta_bytes,
                 "algorithmic_bytes": "8 (offsets) + header + Metadata tail read; 352 row + 32 info "
@@ -816,22 +816,43 @@ def pmc_traffic(workload, kernel_prefix):
     return None
 
 
-def copy_peak_gbs(dev, nbytes=4 << 30, reps=5):
-    """Achievable HBM copy rate on this device (torch copy_), read+write bytes."""
+def hbm_probe(codec, dev, nbytes=4 << 30, reps=5):
+    """The part's achievable streaming rates, measured in this process with the
+    library's own probe kernels (honu_hbm_probe: 16 B per lane, the layout of
+    tools/hbm_probe.hip and of the guide's float4 copy): read-only, write-only
+    and copy (per-wave ranges and grid-stride, 1/2/4 workgroups per CU; the
+    best copy is `copy_gbs`, the roofline's achievable denominator). Copy rates
+    count read + write bytes."""
+    from honu_amd import _lib
+    L, c = codec.lib, codec.ctx
+    s = torch.cuda.current_stream(dev).cuda_stream
     a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     b = torch.empty_like(a)
-    b.copy_(a)
-    torch.cuda.synchronize()
+    a.fill_(1)
+    b.fill_(2)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize()
-    t = e0.elapsed_time(e1) / 1e3 / reps
+
+    def rate(mode, bpc):
+        run = lambda: _lib.check(L.honu_hbm_probe(c, mode, a.data_ptr(), b.data_ptr(), nbytes, bpc, s),  # noqa: E731
+                                 "hbm_probe")
+        run()
+        e0.record()
+        for _ in range(reps):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / 1e3 / reps
+        return (2 if mode >= 2 else 1) * nbytes / t / 1e9
+
+    out = {"bytes": nbytes, "reps": reps}
+    out["read_gbs"] = max(rate(0, k) for k in (1, 2, 4))
+    out["write_gbs"] = max(rate(1, k) for k in (1, 2, 4))
+    best = max(((rate(m, k), m, k) for m in (2, 3) for k in (1, 2, 4)), key=lambda x: x[0])
+    out["copy_gbs"], out["copy_form"] = best[0], (
+        f"{'wave ranges' if best[1] == 2 else 'grid stride'}, {best[2]} workgroups per CU")
     del a, b
     torch.cuda.empty_cache()
-    return 2 * nbytes / t / 1e9
+    return out
 
 
 def _oracle_threads():
@@ -1234,7 +1255,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
     verified = None if args.no_verify else bench.verify()
     zc = bench.zero_copy_decode()
     ok_all = all_ok(verified)
-    peak_meas = copy_peak_gbs(bench.dev)
+    probe = hbm_probe(bench.codec, bench.dev)
     # the legs after the timed steps: none of them changes the numbers above
     bench.payload = None  # the scatter leg keeps the output slots, nothing else
     gc.collect()
@@ -1253,6 +1274,10 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
                                                           all_ok)
     if rank != 0:
         return None
+    if decode is not None and decode.get("materialising") is not None:  # the copy's achievable rate too
+        mr = decode["materialising"]["roofline"]
+        mr["achievable"] = probe["copy_gbs"]
+        mr["frac_of_achievable"] = mr["achieved"] / probe["copy_gbs"]
     step_s = elapsed / args.steps
     total_bytes, total_records = tot
     launches = len(dec_ms)
@@ -1307,6 +1332,8 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": dom_gbs / HBM_PEAK_GBS,
+            "achievable": probe["copy_gbs"],
+            "frac_of_achievable": dom_gbs / probe["copy_gbs"],
             "traffic": traffic,
             "traffic_source": "profiles/pmc_traffic.json" if traffic else None,
             "launches": launches,
@@ -1319,7 +1346,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
             "encode_copy_ms_per_step": sum(enc_ms) / args.steps,
             "decode_copy_ms_per_step": sum(dec_ms) / args.steps,
             "step_hbm_gbs_algorithmic": 4 * bench.total_rec_bytes / step_s / 1e9,
-            "copy_peak_measured_gbs": peak_meas,
+            "hbm_probe": probe,
             "zero_copy_decode_records_per_s": zc["records_per_s"],
             "zero_copy_decode_ms_per_chunk": zc["ms"],
             "zero_copy_decode_chunk_records": zc["records"],

@@ -78,6 +78,7 @@ _PROTOS = {
     "honu_gen_payload": (I32, [P, U64, U64, U64, P, P, P]),
     "honu_digest_records": (I32, [P, P, P, P, U64, P, P]),
     "honu_digest_host": (U64, [P, U64]),
+    "honu_hbm_probe": (I32, [P, I32, P, P, U64, C.c_uint32, P]),
     "honu_verify_decoded": (I32, [P, P, P, P, P, P, P, P, P, P, P, U64, P, P]),
     "honu_host_alloc": (P, [U64]),
     "honu_host_free": (None, [P]),

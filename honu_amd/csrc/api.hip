@@ -19,7 +19,7 @@ struct honu_ctx {
     void *ws;
     uint64_t *counts;        // 3 * max_n
     uint64_t *offs;          // 3 * max_n
-    uint64_t *totals;        // 4
+    uint64_t *totals;        // 4 (3: decode totals; word 3: the HBM probe's sink)
     DecodeScratch *scratch;  // max_n
     uint32_t *reg_inline;    // 8 * max_n: region ids handed from the group parse to fill
     uint64_t *enc_acl;       // max_n: ACL list positions, lane encoder -> group ACL encoder
@@ -137,7 +137,8 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->geom.copy_blocks = env_int("HONU_COPY_BLOCKS", prop.multiProcessorCount * 2);
     c->geom.copy_variant = HONU_AB_BUILD ? env_int("HONU_COPY_VARIANT", 0) : 0;
     c->geom.record_variant = env_int("HONU_RECORD_VARIANT", 0);
-    c->geom.encode_variant = env_int("HONU_ENCODE_VARIANT", 0) == 1 ? 1 : 0;  // 0 default
+    c->geom.encode_variant = env_int("HONU_ENCODE_VARIANT", 0);  // 0 default
+    if (c->geom.encode_variant < 0 || c->geom.encode_variant > 2) c->geom.encode_variant = 0;
     if (c->geom.record_variant != 5 && c->geom.record_variant != 6)
         c->geom.record_variant = 0;
     const uint64_t n = c->max_n;
@@ -145,7 +146,10 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     const uint64_t map_cap = HONU_AB_BUILD ? 1ull << 22 : 0;  // tile map (A/B sweep copy)
     const uint64_t tiles = (n + HONU_WAVE - 1) / HONU_WAVE;
     const uint64_t scan_words = scan_status_words(n);
-    const uint64_t lb_bytes = 2 * sizeof(LbState) + 8 * (3 * tiles + scan_words);
+    // 3 status words per tile, then 3 per 64-tile group (static-tile launches,
+    // lookback.h lb_resolve_grouped)
+    const uint64_t lb_dec_words = 3 * tiles + 3 * LB_GROUPS;
+    const uint64_t lb_bytes = 2 * sizeof(LbState) + 8 * (lb_dec_words + scan_words);
     const uint64_t bytes = 8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 32 * n +
                            8 * n + 4 * map_cap + lb_bytes + 256;
     if (hipMalloc(&c->ws, bytes) != hipSuccess) {
@@ -170,7 +174,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->lb_dec = (LbState *)(c->geom.tile_map + map_cap);
     c->scan.lb = c->lb_dec + 1;
     c->lb_dec_status = (uint64_t *)(c->scan.lb + 1);
-    c->lb_dec_words = 3 * tiles;
+    c->lb_dec_words = lb_dec_words;
     c->scan.status = c->lb_dec_status + c->lb_dec_words;
     c->scan.words = scan_words;
     c->scan.max_blocks = 4 * prop.multiProcessorCount;
@@ -215,7 +219,7 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
     else if (!strcmp(name, "lane_blocks") && value >= 0) ctx->geom.lane_blocks = (int)value;
     else if (!strcmp(name, "copy_variant") && value >= 0 && (value == 0 || HONU_AB_BUILD))
         ctx->geom.copy_variant = (int)value;
-    else if (!strcmp(name, "encode_variant") && (value == 0 || value == 1))
+    else if (!strcmp(name, "encode_variant") && value >= 0 && value <= 2)
         ctx->geom.encode_variant = (int)value;
     else if (!strcmp(name, "record_variant") &&
              (value == 0 || value == 5 || value == 6))
@@ -270,11 +274,13 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
     // encode_variant 0 (default, measured faster: DESIGN §3): header + tail
     // with the ACL lists' partial end chunks (one record per lane), then the
     // lists' whole chunks (16 lanes per record)
+    const int acl_in = ctx->geom.encode_variant == 2;  // the lists' whole chunks in the same kernel
     HIPCHK(launch_encode_meta_lane(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
-                                   out_cap, d_out_off, d_status, ctx->enc_acl,
+                                   out_cap, d_out_off, d_status, ctx->enc_acl, acl_in,
                                    ctx->geom.lane_blocks, (hipStream_t)stream));
-    HIPCHK(launch_encode_acl_grp(d_meta, d_acl, n, d_out, d_status, ctx->enc_acl,
-                                 ctx->geom.lane_blocks, (hipStream_t)stream));
+    if (!acl_in)
+        HIPCHK(launch_encode_acl_grp(d_meta, d_acl, n, d_out, d_status, ctx->enc_acl,
+                                     ctx->geom.lane_blocks, (hipStream_t)stream));
     return HONU_OK;
 }
 
@@ -595,6 +601,19 @@ int32_t honu_gen_payload(honu_ctx *ctx, uint64_t seed, uint64_t first, uint64_t 
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(launch_gen_payload(ctx->geom, seed, first, n, d_payload_off, d_payload,
                               (hipStream_t)stream));
+    return HONU_OK;
+}
+
+int32_t honu_hbm_probe(honu_ctx *ctx, int32_t mode, const void *d_src, void *d_dst, uint64_t bytes,
+                       uint32_t blocks_per_cu, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (mode < 0 || mode > 3) return arg_fail("mode");
+    if (!aligned(d_src, 16) || !aligned(d_dst, 16) || (mode != 1 && !d_src) || (mode != 0 && !d_dst))
+        return arg_fail("buffers must be non-null and 16-byte aligned");
+    if (!blocks_per_cu) blocks_per_cu = 2;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_hbm_probe(mode, d_src, d_dst, bytes, blocks_per_cu * (uint32_t)ctx->geom.num_cu,
+                            reinterpret_cast<uint32_t *>(ctx->totals + 3), (hipStream_t)stream));
     return HONU_OK;
 }
 

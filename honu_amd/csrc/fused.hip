@@ -227,8 +227,11 @@ struct SpecPub {
 
 // MODE 0: plain; 1: speculative publish; 2: guarded recovery (runs only when
 // the speculative launch before it raised misspec). Three instantiations, so
-// profiles tell the launches apart.
-template <int MODE>
+// profiles tell the launches apart. STAT: every tile has a resident wave of
+// its own (tiles <= waves, known at launch): static tiles and grouped prefixes
+// instead of tickets and the decoupled look-back (lookback.h); a kernel of its
+// own, so neither form pays the other's registers.
+template <int MODE, bool STAT>
 __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
     DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t lb_words) {
@@ -248,7 +251,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     // look-back wait, to overlap them with it, doubled the wait: tiles are
     // then handed out ~40 us before their waves start them, which spreads the
     // publish times of consecutive tiles)
-    const bool stat_idx = ntiles <= waves;
+    constexpr bool stat_idx = STAT;
     uint64_t k_static = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + threadIdx.x / HONU_WAVE;
     WSTAMP_START();
     // ticket mode: the next tile's ticket is requested once the current tile's
@@ -260,7 +263,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     // Large 0.258 -> 0.238 ms, profiles/r03/ab/wg_ticket_ab.jsonl).
     uint32_t tk = 0;
     bool tk_pending = false;
-    if (!stat_idx) {  // wave-uniform, and the same in every wave of the workgroup
+    if constexpr (!stat_idx) {  // the same in every wave of the workgroup
         if (threadIdx.x == 0)
             wg_ticket = __hip_atomic_fetch_add(&lb->ticket, (uint32_t)HONU_WAVES_PER_BLOCK, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT);
@@ -270,7 +273,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     }
     for (;;) {
         uint64_t t;
-        if (stat_idx) {
+        if constexpr (stat_idx) {
             t = k_static;
             k_static += waves;
         } else if (tk_pending) {
@@ -324,7 +327,10 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         S.init(fl, P.acl_pos & GRP_POS_MASK, P.nacl);
         if (S.more()) S.issue(ws, rec);
         WSTAMP(10);  // publish + rows out + first staging round issued
-        lb_resolve<3>(lb_status, t, ep, agg, excl);
+        if constexpr (STAT)  // every tile runs at once: grouped prefixes (lookback.h)
+            lb_resolve_grouped<3>(lb_status, lb_status + lb_words - 3 * LB_GROUPS, t, ntiles, ep, agg, excl);
+        else
+            lb_resolve<3>(lb_status, t, ep, agg, excl);
         WSTAMP(11);  // look-back wait
         if (t == ntiles - 1 && lane < 3)
             O.totals[lane] = lane == 0 ? excl[0] + agg[0] : (lane == 1 ? excl[1] + agg[1] : excl[2] + agg[2]);
@@ -466,17 +472,24 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
     // ms with the publish alone, -> 0.778 with the ACL flags too) and, since
     // the flag gather is gone, in static-tile launches of ~1000 tiles and more
     // (profiles/r03/fused_spec_ab.jsonl, spec_acl_ab*.jsonl)
+    const bool stat = tiles <= b * HONU_WAVES_PER_BLOCK && tiles <= (uint64_t)HONU_WAVE * LB_GROUPS;
+    const dim3 grid((unsigned)b), block(HONU_BLOCK);
+#define HONU_FUSED_LAUNCH(M)                                                                               \
+    do {                                                                                                   \
+        if (stat) hipLaunchKernelGGL((k_decode_fused<M, true>), grid, block, 0, s, rec, rec_off, n, O, lb,  \
+                                     lb_status, lb_words);                                                 \
+        else hipLaunchKernelGGL((k_decode_fused<M, false>), grid, block, 0, s, rec, rec_off, n, O, lb,      \
+                                lb_status, lb_words);                                                      \
+    } while (0)
     if (tiles < FUSED_SPEC_MIN_TILES) {
-        hipLaunchKernelGGL(k_decode_fused<0>, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off,
-                           n, O, lb, lb_status, lb_words);
+        HONU_FUSED_LAUNCH(0);
         return hipGetLastError();
     }
     // speculative launch, then the guarded recovery launch (a no-op unless a
     // record failed after publishing its counts: malformed input only)
-    hipLaunchKernelGGL(k_decode_fused<1>, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
-                       O, lb, lb_status, lb_words);
-    hipLaunchKernelGGL(k_decode_fused<2>, dim3((unsigned)b), dim3(HONU_BLOCK), 0, s, rec, rec_off, n,
-                       O, lb, lb_status, lb_words);
+    HONU_FUSED_LAUNCH(1);
+    HONU_FUSED_LAUNCH(2);
+#undef HONU_FUSED_LAUNCH
     return hipGetLastError();
 }
 

@@ -84,7 +84,8 @@ struct LaunchGeom {
                             // (0: one block per 256 lanes of work, no cap)
     int copy_blocks;        // blocks of the byte-balanced copy kernel
     int copy_variant;       // copy engine variant (copy.hip: unroll depth / cache policy)
-    int encode_variant;     // header/tail encoder: 0 lane writer + ACL group kernel
+    int encode_variant;     // header/tail encoder: 0 lane writer + ACL group kernel, 1 group encoder
+                            // (enc.hip), 2 lane writer with the ACL lists in the same kernel
                             // (lane.hip, grp.hip; default), 1 group layout (enc.hip)
     int record_variant;     // per-record kernels: 0 auto (the fastest measured form
                             // of each; honu_decode_batch single-launch from 48 K
@@ -113,7 +114,8 @@ hipError_t launch_decode_keys(const LaunchGeom &g, const honu_meta *meta,
 hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
                                    const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
                                    uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
-                                   int32_t *status, uint64_t *acl_out, int max_blocks, hipStream_t s);
+                                   int32_t *status, uint64_t *acl_out, int acl_in, int max_blocks,
+                                   hipStream_t s);
 hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uint64_t n,
                                  uint8_t *out, const int32_t *status, const uint64_t *acl_pos,
                                  int max_blocks, hipStream_t s);
@@ -190,6 +192,8 @@ uint64_t scan_status_words(uint64_t n);
 hipError_t launch_scan(const uint64_t *in, uint64_t n, int K, uint64_t *out, uint64_t *totals,
                        const ScanState &S, hipStream_t s);
 
+hipError_t launch_hbm_probe(int mode, const void *src, void *dst, uint64_t bytes, uint32_t blocks,
+                            uint32_t *sink, hipStream_t s);
 hipError_t launch_gen_payload(const LaunchGeom &g, uint64_t seed, uint64_t first, uint64_t n,
                               const uint64_t *payload_off, uint8_t *payload, hipStream_t s);
 hipError_t launch_verify_decoded(const LaunchGeom &g, const honu_meta *src, const uint8_t *var,

@@ -141,6 +141,54 @@ HONU_DEV void lb_resolve(uint64_t *status, uint64_t t, uint32_t ep, const uint64
         if (lane == (uint32_t)c) lb_store(status + t * K + c, lb_word(2, ep, excl[c] + agg[c]));
 }
 
+// lb_resolve for launches whose tiles all run at once (static tiles, at most
+// LB_GROUPS x 64 tiles). There the decoupled look-back is slow for late
+// tiles: every tile publishes its aggregate at about the same time, and the
+// inclusive prefixes appear 64 tiles per round trip, so tile t sums back over
+// t / 64 windows, one round trip each (~16 for the last tile of a 1,000-tile
+// launch). Here tiles are grouped by 64: a tile reads its group's earlier
+// aggregates and the previous groups' totals in ONE batch of loads (two per
+// lane per column) and spins only on words not yet published; the group's last
+// tile publishes the group total (status words gstatus[g * K + c], tagged like
+// the tile words) as soon as its group's aggregates are in, before it looks at
+// earlier groups, so no total waits on another: a prefix is two round trips
+// after the aggregates. Tile words keep their aggregates (no inclusive
+// prefixes are written).
+constexpr uint32_t LB_GROUPS = 64;
+template <int K>
+HONU_DEV void lb_resolve_grouped(uint64_t *status, uint64_t *gstatus, uint64_t t, uint64_t ntiles,
+                                 uint32_t ep, const uint64_t (&agg)[K], uint64_t (&excl)[K]) {
+    const uint32_t lane = lane_id();
+    const uint64_t g = t / HONU_WAVE, r = t % HONU_WAVE;
+    const bool closer = r == HONU_WAVE - 1 && t + 1 < ntiles;  // the last group's total is not needed
+    // wave-uniform bit masks of the parts still missing: bit c this group's
+    // tiles before t (r of them), bit K + c the totals of groups 0 .. g - 1
+    uint32_t todo = (1u << K) - 1;
+    if (g) todo |= ((1u << K) - 1) << K;
+#pragma unroll
+    for (int c = 0; c < K; c++) excl[c] = 0;
+    for (;;) {
+#pragma unroll
+        for (int c = 0; c < 2 * K; c++) {
+            if (!(todo & (1u << c))) continue;
+            const bool grp = c >= K;
+            const int col = grp ? c - K : c;
+            const uint64_t n_in = grp ? g : r;
+            const uint64_t *src = grp ? gstatus + (uint64_t)lane * K + col
+                                      : status + (g * HONU_WAVE + lane) * K + col;
+            const uint64_t w = lane < n_in ? lb_load(src) : lb_word(1, ep, 0);
+            const bool ready = (w >> 62) != 0 && ((uint32_t)(w >> 44) & LB_EPOCH_MASK) == (ep & LB_EPOCH_MASK);
+            if (__ballot(!ready)) continue;
+            const uint64_t sum = wave_sum(w & LB_VAL_MASK);
+            excl[col] += sum;
+            todo &= ~(1u << c);
+            if (!grp && closer && lane == 0) lb_store(gstatus + g * K + col, lb_word(1, ep, sum + agg[col]));
+        }
+        if (!todo) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 // The scans' end (scan.hip; the single-launch decode ends in lb_finish_blocks).
 // Called by every wave with the ticket that ended its loop (t_end >= ntiles):
 // a wave takes that ticket only after finishing its last tile, so the wave

@@ -198,6 +198,68 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_verify_decoded(
     }
 }
 
+// ------------------------------------------------------------------------
+// HBM probe (honu_hbm_probe): the part's achievable streaming rates, for the
+// bench's roofline denominator next to the 8 TB/s spec. 16 bytes per lane,
+// each wave a contiguous range (the layout of the codec's copy engine) with 8
+// chunks per lane in flight, or grid-stride with 4 (the guide's float4 copy).
+// ------------------------------------------------------------------------
+template <int MODE>  // 0 read, 1 write, 2 copy (wave ranges), 3 copy (grid stride)
+__global__ __launch_bounds__(HONU_BLOCK) void k_hbm_probe(const u32x4 *__restrict__ a, u32x4 *__restrict__ b,
+                                                          uint64_t n, uint32_t *__restrict__ sink) {
+    const uint32_t lane = lane_id();
+    if constexpr (MODE == 3) {
+        constexpr int U = 4;
+        const uint64_t stride = (uint64_t)gridDim.x * HONU_BLOCK * U;
+        for (uint64_t i = (uint64_t)blockIdx.x * HONU_BLOCK * U + threadIdx.x; i < n; i += stride) {
+            u32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (i + u * HONU_BLOCK < n) v[u] = a[i + u * HONU_BLOCK];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (i + u * HONU_BLOCK < n) b[i + u * HONU_BLOCK] = v[u];
+        }
+        return;
+    }
+    constexpr int U = 8;
+    const uint64_t W = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
+    const uint64_t w = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + threadIdx.x / HONU_WAVE;
+    const uint64_t lo = n * w / W, hi = n * (w + 1) / W;
+    u32x4 acc = {0, 0, 0, 0};
+    for (uint64_t i = lo + lane; i < hi; i += (uint64_t)HONU_WAVE * U) {
+        u32x4 v[U];
+        if constexpr (MODE != 1) {
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (i + u * HONU_WAVE < hi) v[u] = a[i + u * HONU_WAVE];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (i + u * HONU_WAVE >= hi) continue;
+            if constexpr (MODE == 0) acc ^= v[u];
+            else if constexpr (MODE == 1) b[i + u * HONU_WAVE] = u32x4{(uint32_t)i, (uint32_t)u, 1, 2};
+            else b[i + u * HONU_WAVE] = v[u];
+        }
+    }
+    if constexpr (MODE == 0)
+        if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u) sink[0] = 1;  // keeps the loads
+}
+
+hipError_t launch_hbm_probe(int mode, const void *src, void *dst, uint64_t bytes, uint32_t blocks,
+                            uint32_t *sink, hipStream_t s) {
+    const uint64_t n = bytes / 16;
+    const u32x4 *a = reinterpret_cast<const u32x4 *>(src);
+    u32x4 *b = reinterpret_cast<u32x4 *>(dst);
+    switch (mode) {
+    case 0: hipLaunchKernelGGL(k_hbm_probe<0>, dim3(blocks), dim3(HONU_BLOCK), 0, s, a, b, n, sink); break;
+    case 1: hipLaunchKernelGGL(k_hbm_probe<1>, dim3(blocks), dim3(HONU_BLOCK), 0, s, a, b, n, sink); break;
+    case 2: hipLaunchKernelGGL(k_hbm_probe<2>, dim3(blocks), dim3(HONU_BLOCK), 0, s, a, b, n, sink); break;
+    default: hipLaunchKernelGGL(k_hbm_probe<3>, dim3(blocks), dim3(HONU_BLOCK), 0, s, a, b, n, sink); break;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_gen_payload(const LaunchGeom &g, uint64_t seed, uint64_t first, uint64_t n,
                               const uint64_t *payload_off, uint8_t *payload, hipStream_t s) {
     if (n == 0) return hipSuccess;

@@ -324,7 +324,13 @@ int32_t honu_decode_payloads(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n,
  * against data_cap) and honu_decode_payloads (same context, same d_totals)
  * then copies the payloads; with materialize == 0 Data() stays the zero-copy
  * subslice of the records arena (Object.Data, object.go:85-99). Results are
- * identical to the split path's. */
+ * identical to the split path's. Launches of 768 or more 64-record tiles
+ * speculate (counts published before the walk ends, ACL entry flags checked
+ * by the table fill); a batch holding any record that fails after its counts
+ * were published, or a nil ACL entry, is decoded a second time without
+ * speculation inside the same call, so such a batch costs about twice a
+ * clean one (malformed input and nil entries only; results are exact either
+ * way). */
 int32_t honu_decode_records(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
                             uint64_t n, honu_meta *d_meta, honu_record_info *d_info,
                             honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,
@@ -690,6 +696,16 @@ int32_t honu_verify_decoded(honu_ctx *ctx, const honu_meta *d_src, const uint8_t
                             uint32_t *d_mismatch, void *stream);
 /* The same digest of one host byte run. */
 uint64_t honu_digest_host(const uint8_t *p, uint64_t len);
+
+/* Measurement: the part's achievable HBM streaming rates (bench.py's
+ * roofline denominator beside the 8 TB/s spec). mode 0 reads bytes of d_src,
+ * 1 writes bytes of d_dst, 2 copies d_src -> d_dst with each wave on a
+ * contiguous range (the codec copy engine's layout, 8 x 16 B per lane in
+ * flight), 3 the same copy grid-stride (4 x 16 B per lane). bytes is rounded
+ * down to 16; buffers 16-byte aligned; blocks_per_cu 0 = 2. Asynchronous on
+ * stream; time it with events. */
+int32_t honu_hbm_probe(honu_ctx *ctx, int32_t mode, const void *d_src, void *d_dst, uint64_t bytes,
+                       uint32_t blocks_per_cu, void *stream);
 
 /* ------------------------------------------------------------------------ */
 /* Host memory helpers (pinned buffers for the host<->device path)          */

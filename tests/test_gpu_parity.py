@@ -21,13 +21,14 @@ from honu_amd.metadata import META_DTYPE, normalize, pack_batch, unpack_row  # n
 from honu_amd.workload import gen_host_batch, gen_meta  # noqa: E402
 
 
-@pytest.fixture(scope="module", params=[(6, 0), (5, 1)], ids=["fused", "split"])
+@pytest.fixture(scope="module", params=[(6, 0), (5, 1), (6, 2)], ids=["fused", "split", "acl_in"])
 def codec(request):
-    """Both metadata decodes and both header/tail encoders of the product
+    """Both metadata decodes and the three header/tail encoders of the product
     library: the single-launch decode (fused.hip) at every batch size with the
-    default lane encoder + group ACL lists (lane.hip, grp.hip), and the split
+    default lane encoder + group ACL lists (lane.hip, grp.hip), the split
     decode kernels (windowed lane parse, group fill) with the group-layout
-    encoder (enc.hip, encode_variant 1). The default picks the decode by batch
+    encoder (enc.hip, encode_variant 1), and the lane encoder writing the ACL
+    lists itself (encode_variant 2). The default picks the decode by batch
     size; the bench pipeline and large-batch tests run it."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -297,7 +298,8 @@ def test_long_tails_and_nil_entries_parity(codec, oracle_lib):
 
 
 @pytest.mark.parametrize("lens", ["tiny", "edges", "skew"])
-@pytest.mark.parametrize("copy_variant", [0, 1, 6, 11, 12, 13], ids=["default", "unroll8", "sweep", "nt_load", "nt_store", "unaligned"])
+@pytest.mark.parametrize("copy_variant", [0, 1, 6, 11, 12, 13, 16, 17],
+                         ids=["default", "unroll8", "sweep", "nt_load", "nt_store", "unaligned", "dpp", "dpp8"])
 def test_copy_engine_parity(oracle_lib, copy_variant, lens):
     """The payload copy engine on awkward length mixes: payloads of 0-40 bytes
     (head/tail bytes only), lengths around multiples of 16, and a skewed mix of
@@ -623,3 +625,25 @@ def test_encode_writer_drain_bounds(codec, oracle_lib):
     oout, ooff, ost = oracle_lib.marshal_batch(hb)
     assert np.array_equal(st, ost) and (st == 0).all()
     assert np.array_equal(off, ooff) and out.tobytes() == oout.tobytes()
+
+
+def test_hbm_probe_modes(codec):
+    """honu_hbm_probe (bench.py's achievable-rate denominator): both copy forms
+    move every byte (sizes not a multiple of a wave's chunk), the write form
+    fills the buffer, bad arguments are refused."""
+    L = hobj._lib
+    for nbytes in (16, 4096 + 48, (3 << 20) + 16 * 77):
+        a = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device=codec.torch_device)
+        for mode in (2, 3):
+            for bpc in (0, 1, 4):
+                b = torch.zeros_like(a)
+                L.check(codec.lib.honu_hbm_probe(codec.ctx, mode, L.ptr(a), L.ptr(b), nbytes, bpc,
+                                                 codec.stream), "probe")
+                torch.cuda.synchronize()
+                assert torch.equal(a, b), (nbytes, mode, bpc)
+        b = torch.zeros_like(a)
+        L.check(codec.lib.honu_hbm_probe(codec.ctx, 1, None, L.ptr(b), nbytes, 2, codec.stream), "probe")
+        L.check(codec.lib.honu_hbm_probe(codec.ctx, 0, L.ptr(a), None, nbytes, 2, codec.stream), "probe")
+        torch.cuda.synchronize()
+        assert int((b.view(torch.int32)[2::4] == 1).sum()) == nbytes // 16
+    assert codec.lib.honu_hbm_probe(codec.ctx, 7, None, None, 16, 1, codec.stream) != 0

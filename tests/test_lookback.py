@@ -310,10 +310,12 @@ def test_speculated_long_list_checked_under_capacity_failure(oracle_lib):
         tot = d.tot[:24].cpu().numpy().view(np.uint64)
         assert np.array_equal(tot, otot)
         assert d.meta[:352 * n].cpu().numpy().tobytes() == ometa.tobytes()
-        info = np.frombuffer(d.info[:32 * n].cpu().numpy().tobytes(), oinfo.dtype)
-        want = oinfo.copy()
-        want["meta_status"][-1] = 9  # HONU_ERR_CAPACITY
-        assert info.tobytes() == want.tobytes()
+        # raw bytes (a numpy copy of a structured array need not keep its pad
+        # bytes): the last record's meta_status (byte 20 of its 32) is CAPACITY
+        want = bytearray(oinfo.tobytes())
+        ms = oinfo.dtype.fields["meta_status"][1]
+        want[32 * (n - 1) + ms:32 * (n - 1) + ms + 4] = (9).to_bytes(4, "little")  # HONU_ERR_CAPACITY
+        assert d.info[:32 * n].cpu().numpy().tobytes() == bytes(want)
         nacl = int(otot[0]) - 1200  # the entries of every record before the last
         assert d.acl[:20 * nacl].cpu().numpy().tobytes() == oacl[:nacl].tobytes()
         nreg = int(otot[1]) - 5  # the capacity-failed record stores no regions either

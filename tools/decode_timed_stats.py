@@ -26,7 +26,7 @@ def main():
         rows = sorted(csv.DictReader(f), key=lambda r: int(r["Start_Timestamp"]))
     dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6  # noqa: E731
     out = {"bench": bench}
-    g = [r for r in rows if "k_decode_fused<2>" in r["Kernel_Name"]]
+    g = [r for r in rows if "k_decode_fused<2" in r["Kernel_Name"]]
     if g:
         out["guarded_launches"] = {"count": len(g),
                                    "avg_us": sum(dur(r) for r in g) / len(g) * 1e3}
@@ -34,8 +34,8 @@ def main():
     if zc:
         # the speculative launches (k_decode_fused<1>; each is followed by a
         # guarded <2> that returns at once), else the plain ones (<0>)
-        fused = [r for r in rows if "k_decode_fused<1>" in r["Kernel_Name"]] or \
-            [r for r in rows if "k_decode_fused<0>" in r["Kernel_Name"]]
+        fused = [r for r in rows if "k_decode_fused<1" in r["Kernel_Name"]] or \
+            [r for r in rows if "k_decode_fused<0" in r["Kernel_Name"]]
         reps = zc["reps"]
         timed = fused[1:1 + reps]
         ms = sum(dur(r) for r in timed) / len(timed)
