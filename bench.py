@@ -75,7 +75,8 @@ def parse_args(argv=None):
                    help="workgroups per CU for the lane/group metadata kernels while copies run "
                         "beside them (0 = no cap; -1 = auto: 2 when records average > 64 KiB, "
                         "where the copies dominate, else no cap)")
-    p.add_argument("--copy-prio", type=int, default=1, help="copy stream gets high priority")
+    p.add_argument("--copy-prio", type=int, default=1,
+                   help="1: the copy stream gets high priority; 0: neither; -1: the metadata stream does")
     p.add_argument("--meta-beside", choices=["auto", "encode", "decode"], default="auto",
                    help="chunk k+1's metadata kernels start when its slot frees (beside chunk "
                         "k's encode copy) or once chunk k's encode copy is done (beside its "
@@ -222,9 +223,9 @@ class Bench:
                                                            args.meta_blocks * ncu), "param")
                 _lib.check(self.lib.honu_ctx_set_param(sl.codec.ctx, b"lane_blocks",
                                                        self.lane_blocks * ncu), "param")
-        self.sm = torch.cuda.Stream(self.dev)  # metadata kernels
+        self.sm = torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio < 0 else 0)  # metadata kernels
         # payload copies: the bandwidth-bound critical path, dispatched first
-        self.sc = (torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio else 0)
+        self.sc = (torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio > 0 else 0)
                    if nslots == 2 else self.sm)
         if args.meta_cu_stride and nslots == 2:  # metadata and copies on their own CUs
             S = args.meta_cu_stride

@@ -27,7 +27,8 @@ struct honu_ctx {
     // ticket/epoch block and 3 status words per 64-record tile
     LbState *lb_dec;
     uint64_t *lb_dec_status;
-    uint64_t lb_dec_words;
+    uint64_t *lb_dec_gstatus;  // the group words, after the tile words (same epoch scheme)
+    uint64_t lb_dec_words;     // tile + group words
     uint64_t lb_bytes;       // the look-back blocks + status words, from lb_dec
     ScanState scan;          // look-back state of the one-launch scans (scan.hip)
 };
@@ -137,8 +138,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->geom.copy_blocks = env_int("HONU_COPY_BLOCKS", prop.multiProcessorCount * 2);
     c->geom.copy_variant = HONU_AB_BUILD ? env_int("HONU_COPY_VARIANT", 0) : 0;
     c->geom.record_variant = env_int("HONU_RECORD_VARIANT", 0);
-    c->geom.encode_variant = env_int("HONU_ENCODE_VARIANT", 0);  // 0 default
-    if (c->geom.encode_variant < 0 || c->geom.encode_variant > 2) c->geom.encode_variant = 0;
+    c->geom.encode_variant = env_int("HONU_ENCODE_VARIANT", 0) == 1 ? 1 : 0;  // 0 default
     if (c->geom.record_variant != 5 && c->geom.record_variant != 6)
         c->geom.record_variant = 0;
     const uint64_t n = c->max_n;
@@ -146,9 +146,10 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     const uint64_t map_cap = HONU_AB_BUILD ? 1ull << 22 : 0;  // tile map (A/B sweep copy)
     const uint64_t tiles = (n + HONU_WAVE - 1) / HONU_WAVE;
     const uint64_t scan_words = scan_status_words(n);
-    // 3 status words per tile, then 3 per 64-tile group (static-tile launches,
-    // lookback.h lb_resolve_grouped)
-    const uint64_t lb_dec_words = 3 * tiles + 3 * LB_GROUPS;
+    // 3 status words per tile, then 3 per 64-tile group (lookback.h
+    // lb_resolve_grouped*)
+    const uint64_t groups = (tiles / HONU_WAVE + 1) > LB_GROUPS ? tiles / HONU_WAVE + 1 : LB_GROUPS;
+    const uint64_t lb_dec_words = 3 * tiles + 3 * groups;
     const uint64_t lb_bytes = 2 * sizeof(LbState) + 8 * (lb_dec_words + scan_words);
     const uint64_t bytes = 8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 32 * n +
                            8 * n + 4 * map_cap + lb_bytes + 256;
@@ -175,6 +176,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->scan.lb = c->lb_dec + 1;
     c->lb_dec_status = (uint64_t *)(c->scan.lb + 1);
     c->lb_dec_words = lb_dec_words;
+    c->lb_dec_gstatus = c->lb_dec_status + 3 * tiles;
     c->scan.status = c->lb_dec_status + c->lb_dec_words;
     c->scan.words = scan_words;
     c->scan.max_blocks = 4 * prop.multiProcessorCount;
@@ -219,7 +221,7 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
     else if (!strcmp(name, "lane_blocks") && value >= 0) ctx->geom.lane_blocks = (int)value;
     else if (!strcmp(name, "copy_variant") && value >= 0 && (value == 0 || HONU_AB_BUILD))
         ctx->geom.copy_variant = (int)value;
-    else if (!strcmp(name, "encode_variant") && value >= 0 && value <= 2)
+    else if (!strcmp(name, "encode_variant") && (value == 0 || value == 1))
         ctx->geom.encode_variant = (int)value;
     else if (!strcmp(name, "record_variant") &&
              (value == 0 || value == 5 || value == 6))
@@ -274,13 +276,11 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
     // encode_variant 0 (default, measured faster: DESIGN §3): header + tail
     // with the ACL lists' partial end chunks (one record per lane), then the
     // lists' whole chunks (16 lanes per record)
-    const int acl_in = ctx->geom.encode_variant == 2;  // the lists' whole chunks in the same kernel
     HIPCHK(launch_encode_meta_lane(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
-                                   out_cap, d_out_off, d_status, ctx->enc_acl, acl_in,
+                                   out_cap, d_out_off, d_status, ctx->enc_acl,
                                    ctx->geom.lane_blocks, (hipStream_t)stream));
-    if (!acl_in)
-        HIPCHK(launch_encode_acl_grp(d_meta, d_acl, n, d_out, d_status, ctx->enc_acl,
-                                     ctx->geom.lane_blocks, (hipStream_t)stream));
+    HIPCHK(launch_encode_acl_grp(d_meta, d_acl, n, d_out, d_status, ctx->enc_acl,
+                                 ctx->geom.lane_blocks, (hipStream_t)stream));
     return HONU_OK;
 }
 
@@ -409,8 +409,8 @@ int32_t honu_decode_records(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t 
     }
     HIPCHK(launch_decode_fused(d_rec, d_rec_off, n, d_meta, d_info, d_acl, acl_cap, d_regions,
                                regions_cap, materialize != 0, data_cap, ctx->scratch, ctx->offs,
-                               tot, ctx->lb_dec, ctx->lb_dec_status, ctx->lb_dec_words,
-                               fused_blocks(ctx->geom), s));
+                               tot, ctx->lb_dec, ctx->lb_dec_status, ctx->lb_dec_gstatus,
+                               ctx->lb_dec_words, fused_blocks(ctx->geom), s));
     return HONU_OK;
 }
 

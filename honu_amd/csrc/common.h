@@ -216,37 +216,37 @@ HONU_DEV void wave_copy_bytes(uint8_t *__restrict__ dst, const uint8_t *__restri
 // page, so the over-read is always mapped.
 // NT: non-temporal cache policy, 0 none, 1 loads and stores, 2 loads only,
 // 3 stores only; 4: a misaligned source is read with one unaligned 16-byte
-// load per chunk instead of two aligned loads and a funnel; 5: one aligned
-// load per chunk, the funnel's second block from the next lane by a DPP
-// wave shift (lane 63's from lane 0 of the next unrolled chunk row, or one
-// extra load after the last).
+// load per chunk instead of two aligned loads and a funnel; 5 (A/B): one
+// aligned load per chunk, the funnel's second block taken from the next lane
+// by a DPP wave shift (wave_shl:1) - lane 63's from lane 0 of the next
+// unrolled row - and loaded directly only by the last chunk's lane and by
+// lane 63 of the last row: a third fewer load requests through the L1 (the
+// copies run with TA / TD 91-98 % busy, DESIGN §3 "Round 4").
 // The head bytes, the tail bytes and the first UNROLL x 64 chunks are all
 // loaded before any of them is stored, so a short segment (the common case
 // for Small records: 2.5 KB) costs one round trip, not three.
-// wave_copy NT 5: b[u] (the aligned source block after lane l's, i.e. lane
-// l + 1's a[u]) by a DPP wave shift; lane 63 takes lane 0's a[u + 1], and after
-// the last row loads its own (only when the source is misaligned, p != 0)
+// wave_copy NT 5: b[u] (the aligned source block after this lane's chunk)
+// from the next lane's a[u] by a DPP wave shift; lanes that loaded b
+// themselves (own) keep it. All lanes call it (converged).
 template <int UNROLL>
-HONU_DEV void dpp_second(const u32x4 (&a)[UNROLL], u32x4 (&b)[UNROLL], uint64_t c, uint64_t chunks,
-                         const u32x4 *s4, uint32_t p) {
-    if (!p) return;  // wave-uniform
+HONU_DEV void dpp_second(const u32x4 (&a)[UNROLL], u32x4 (&b)[UNROLL], uint64_t c, uint64_t chunks) {
     const uint32_t lane = lane_id();
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
         u32x4 v;
-        v.x = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[u].x, 0x130, 0xF, 0xF, false);  // wave_shl:1
-        v.y = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[u].y, 0x130, 0xF, 0xF, false);
-        v.z = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[u].z, 0x130, 0xF, 0xF, false);
-        v.w = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[u].w, 0x130, 0xF, 0xF, false);
-        if (u + 1 < UNROLL) {
-            const u32x4 &n = a[u + 1 < UNROLL ? u + 1 : u];
-            const uint32_t nx = __builtin_amdgcn_readlane(n.x, 0), ny = __builtin_amdgcn_readlane(n.y, 0);
-            const uint32_t nz = __builtin_amdgcn_readlane(n.z, 0), nw = __builtin_amdgcn_readlane(n.w, 0);
-            if (lane == HONU_WAVE - 1) v = u32x4{nx, ny, nz, nw};
-        } else if (lane == HONU_WAVE - 1 && c + u * HONU_WAVE < chunks) {
-            v = s4[c + u * HONU_WAVE + 1];
+        v.x = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[u].x, 0x130, 0xF, 0xF, true);  // wave_shl:1
+        v.y = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[u].y, 0x130, 0xF, 0xF, true);
+        v.z = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[u].z, 0x130, 0xF, 0xF, true);
+        v.w = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[u].w, 0x130, 0xF, 0xF, true);
+        if (u + 1 < UNROLL) {  // lane 63: lane 0's block of the next row
+            const u32x4 &nx = a[u + 1 < UNROLL ? u + 1 : u];
+            const uint32_t x0 = __builtin_amdgcn_readlane(nx.x, 0), x1 = __builtin_amdgcn_readlane(nx.y, 0);
+            const uint32_t x2 = __builtin_amdgcn_readlane(nx.z, 0), x3 = __builtin_amdgcn_readlane(nx.w, 0);
+            if (lane == HONU_WAVE - 1) v = u32x4{x0, x1, x2, x3};
         }
-        b[u] = v;
+        const uint64_t cu = c + (uint64_t)u * HONU_WAVE;
+        const bool own = cu + 1 >= chunks || (lane == HONU_WAVE - 1 && u == UNROLL - 1);
+        if (cu < chunks && !own) b[u] = v;
     }
 }
 
@@ -264,9 +264,10 @@ HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ s
     const uint8_t *bsrc = src + head;
     const uint32_t p = (uint32_t)((uint64_t)bsrc & 15u);  // wave-uniform
     const u32x4 *__restrict__ s4 = reinterpret_cast<const u32x4 *>(bsrc - p);
-    auto load = [&](uint64_t c, u32x4 &a, u32x4 &b) {
-        if (NT == 5) {
+    auto load = [&](uint64_t c, u32x4 &a, u32x4 &b, int u) {
+        if (NT == 5) {  // the second block only where no neighbour lane holds it
             a = *(&s4[c]);
+            if (p && (c + 1 >= chunks || (lane == HONU_WAVE - 1 && u == UNROLL - 1))) b = s4[c + 1];
             return;
         }
         if (NT == 4 && p) {
@@ -287,8 +288,9 @@ HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ s
         u32x4 a[UNROLL], b[UNROLL];
 #pragma unroll
         for (int u = 0; u < UNROLL; u++)
-            if (lane + u * HONU_WAVE < chunks) load(lane + u * HONU_WAVE, a[u], b[u]);
-        if constexpr (NT == 5) dpp_second(a, b, (uint64_t)lane, chunks, s4, p);
+            if (lane + u * HONU_WAVE < chunks) load(lane + u * HONU_WAVE, a[u], b[u], u);
+        if constexpr (NT == 5)
+            if (p) dpp_second(a, b, (uint64_t)lane, chunks);
         if (lane < head) dst[lane] = hv;
 #pragma unroll
         for (int u = 0; u < UNROLL; u++)
@@ -301,8 +303,9 @@ HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ s
         u32x4 a[UNROLL], b[UNROLL];
 #pragma unroll
         for (int u = 0; u < UNROLL; u++)
-            if (c + u * HONU_WAVE < chunks) load(c + u * HONU_WAVE, a[u], b[u]);
-        if constexpr (NT == 5) dpp_second(a, b, c, chunks, s4, p);
+            if (c + u * HONU_WAVE < chunks) load(c + u * HONU_WAVE, a[u], b[u], u);
+        if constexpr (NT == 5)
+            if (p) dpp_second(a, b, c, chunks);
 #pragma unroll
         for (int u = 0; u < UNROLL; u++)
             if (c + u * HONU_WAVE < chunks) store(c + u * HONU_WAVE, a[u], b[u]);

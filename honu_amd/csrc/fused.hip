@@ -51,6 +51,9 @@ struct DecodeOut {
 // slower); the measurement knobs that skip the fill, the look-back wait or
 // the tickets (HONU_FUSED_DBG). DESIGN §3 has the numbers.
 constexpr uint64_t FUSED_SPEC_MIN_TILES = 768;
+#ifndef FUSED_GROUP_LB
+#define FUSED_GROUP_LB 1
+#endif
 
 // The ACL lists (every entry present) of a tile staged into the wave's LDS
 // (its windows, free after the walk) for the table fill: round after round,
@@ -234,7 +237,7 @@ struct SpecPub {
 template <int MODE, bool STAT>
 __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
-    DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t lb_words) {
+    DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t *lb_gstatus, uint64_t lb_words) {
     constexpr int mode = MODE;
     if (mode == 2 && __hip_atomic_load(&lb->misspec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
         return;  // every wave of the launch returns: the look-back state is untouched
@@ -284,9 +287,10 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         }
         if (t >= ntiles) break;
         const uint64_t i0 = t * HONU_WAVE, i = i0 + lane;
-        const bool valid = i < n;
+        const uint64_t lim = i0 + HONU_WAVE < n ? i0 + HONU_WAVE : n;  // the tile's records are [i0, lim)
+        const bool valid = i < lim;
         TileHead H;
-        tile_head_bounds(i0, rec_off, n, H);
+        tile_head_bounds(i0, rec_off, lim, H);
         tile_head_bytes(rec, H);
         WinParse P;
         RegRow R;
@@ -296,7 +300,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         early.status = lb_status;
         early.t = t;
         early.ep = ep;
-        win_walk(i0, ws, rec, n, H, R, P, early);
+        win_walk(i0, ws, rec, lim, H, R, P, early);
 
         // counts -> offsets: wave scan + look-back across tiles
         uint64_t agg[3], excl[3], x0, x1, x2;
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
             // (their list offsets are patched in below)
             lb_publish<3>(lb_status, t, ep, agg);
         }
-        rows_out(ws, R, i0, n, O.meta);
+        rows_out(ws, R, i0, lim, O.meta);
         // the ACL lists with every entry present go to the table from LDS: the
         // first round of their blocks is staged now, before the wait, as it
         // needs no offsets
@@ -328,7 +332,9 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         if (S.more()) S.issue(ws, rec);
         WSTAMP(10);  // publish + rows out + first staging round issued
         if constexpr (STAT)  // every tile runs at once: grouped prefixes (lookback.h)
-            lb_resolve_grouped<3>(lb_status, lb_status + lb_words - 3 * LB_GROUPS, t, ntiles, ep, agg, excl);
+            lb_resolve_grouped<3>(lb_status, lb_gstatus, t, ntiles, ep, agg, excl);
+        else if constexpr (FUSED_GROUP_LB)  // tickets: a look-back over the group totals
+            lb_resolve_grouped_lb<3>(lb_status, lb_gstatus, t, ntiles, ep, agg, excl);
         else
             lb_resolve<3>(lb_status, t, ep, agg, excl);
         WSTAMP(11);  // look-back wait
@@ -462,8 +468,13 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
                                uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap, int materialize,
                                uint64_t data_cap, DecodeScratch *scratch, uint64_t *offs,
                                uint64_t *totals, LbState *lb, uint64_t *lb_status,
-                               uint64_t lb_words, int max_blocks, hipStream_t s) {
+                               uint64_t *lb_gstatus, uint64_t lb_words, int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
+    // (32-record tiles for batches whose 64-record tiles fill at most half the
+    // resident waves, so that every SIMD walks records, measured slower with
+    // the grouped prefixes too: 62 K Large 0.0742 -> 0.0774 ms, 64 K XLarge
+    // zero copy 0.0766 -> 0.0803 ms; the walk's latency, not the idle SIMDs,
+    // sets a short batch's time. DESIGN §3 "Round 4".)
     const uint64_t tiles = (n + HONU_WAVE - 1) / HONU_WAVE;
     uint64_t b = (tiles + HONU_WAVES_PER_BLOCK - 1) / HONU_WAVES_PER_BLOCK;
     if (max_blocks > 0 && b > (uint64_t)max_blocks) b = (uint64_t)max_blocks;
@@ -477,9 +488,9 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
 #define HONU_FUSED_LAUNCH(M)                                                                               \
     do {                                                                                                   \
         if (stat) hipLaunchKernelGGL((k_decode_fused<M, true>), grid, block, 0, s, rec, rec_off, n, O, lb,  \
-                                     lb_status, lb_words);                                                 \
+                                     lb_status, lb_gstatus, lb_words);                                                 \
         else hipLaunchKernelGGL((k_decode_fused<M, false>), grid, block, 0, s, rec, rec_off, n, O, lb,      \
-                                lb_status, lb_words);                                                      \
+                                lb_status, lb_gstatus, lb_words);                                                      \
     } while (0)
     if (tiles < FUSED_SPEC_MIN_TILES) {
         HONU_FUSED_LAUNCH(0);

@@ -85,7 +85,7 @@ struct LaunchGeom {
     int copy_blocks;        // blocks of the byte-balanced copy kernel
     int copy_variant;       // copy engine variant (copy.hip: unroll depth / cache policy)
     int encode_variant;     // header/tail encoder: 0 lane writer + ACL group kernel, 1 group encoder
-                            // (enc.hip), 2 lane writer with the ACL lists in the same kernel
+                            // (enc.hip)
                             // (lane.hip, grp.hip; default), 1 group layout (enc.hip)
     int record_variant;     // per-record kernels: 0 auto (the fastest measured form
                             // of each; honu_decode_batch single-launch from 48 K
@@ -114,8 +114,7 @@ hipError_t launch_decode_keys(const LaunchGeom &g, const honu_meta *meta,
 hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
                                    const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
                                    uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
-                                   int32_t *status, uint64_t *acl_out, int acl_in, int max_blocks,
-                                   hipStream_t s);
+                                   int32_t *status, uint64_t *acl_out, int max_blocks, hipStream_t s);
 hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uint64_t n,
                                  uint8_t *out, const int32_t *status, const uint64_t *acl_pos,
                                  int max_blocks, hipStream_t s);
@@ -144,7 +143,7 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
                                uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap, int materialize,
                                uint64_t data_cap, DecodeScratch *scratch, uint64_t *offs,
                                uint64_t *totals, LbState *lb, uint64_t *lb_status,
-                               uint64_t lb_words, int max_blocks, hipStream_t s);
+                               uint64_t *lb_gstatus, uint64_t lb_words, int max_blocks, hipStream_t s);
 
 hipError_t launch_decode_parse_win(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                    honu_meta *meta, honu_record_info *info,

@@ -216,11 +216,6 @@ HONU_DEV uint32_t uvarint_bytes(uint64_t x, uint64_t &lo, uint64_t &hi) {
 // places with most lanes active, instead of from every put() with the few
 // lanes whose chunk just filled (42 % fewer store instructions; the encoder
 // is bound by the L1's miss queue, so this bought 1 %: DESIGN §3).
-// ENC_ABL (measurement only, wrong output): 1 frame bodies not loaded, 2 ACL
-// end entries not loaded, 4 regions not loaded, 8 no chunk stores
-#ifndef ENC_ABL
-#define ENC_ABL 0
-#endif
 template <int R>
 struct LaneWriterT {
     uint8_t *out;
@@ -265,7 +260,7 @@ struct LaneWriterT {
             if constexpr (R > 0) {
                 ring[((cpos >> 4) & (R - 1)) * HONU_WAVE] = v;
                 nch++;
-            } else if (!(ENC_ABL & 8)) {
+            } else {
                 *reinterpret_cast<u32x4 *>(out + cpos) = v;
             }
         } else {  // the head chunk: parked until finish()
@@ -324,7 +319,7 @@ struct LaneWriterT {
 #pragma unroll
             for (int j = 0; j < 5; j++) {
                 u32x4 v{0, 0, 0, 0};
-                if (!(ENC_ABL & 1) && q0 + j < nw) v = w[q0 + j];
+                if (q0 + j < nw) v = w[q0 + j];
                 x[2 * j] = ((uint64_t)v.y << 32) | v.x;
                 x[2 * j + 1] = ((uint64_t)v.w << 32) | v.z;
             }
@@ -342,23 +337,6 @@ struct LaneWriterT {
             }
         }
     }
-    // the first n bytes of the word run x (byte phase a in x[0], a < 16;
-    // x holds NW words, the last one zero padding) - run()'s inner loop over
-    // registers: 8 bytes per put, funnel-shifted by the lane's phase
-    template <int NW> HONU_DEV void put_words(const uint64_t (&x)[NW], uint32_t a, uint64_t n) {
-        const uint32_t sh = (a & 7) * 8, hw = a >> 3;
-#pragma unroll
-        for (int j = 0; j + 2 < NW; j++) {
-            const uint64_t off = 8ull * j;
-            if (off < n) {
-                const uint64_t take = n - off < 8 ? n - off : 8;
-                const uint64_t lo = hw ? x[j + 1] : x[j], hi = hw ? x[j + 2] : x[j + 1];
-                uint64_t v = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
-                if (take < 8) v &= (1ull << (8 * take)) - 1;
-                put(v, (uint32_t)take);
-            }
-        }
-    }
     HONU_DEV void frame(const uint8_t *var, honu_span sp) {  // lani Encode :62-77
         uv(sp.len);
         run(var + sp.off, sp.len);
@@ -367,7 +345,7 @@ struct LaneWriterT {
     HONU_DEV void drain() {
         if constexpr (R > 0) {
             const uint64_t p0 = cpos - 16ull * nch;
-            for (uint32_t k = 0; k < nch && !(ENC_ABL & 8); k++)
+            for (uint32_t k = 0; k < nch; k++)
                 *reinterpret_cast<u32x4 *>(out + p0 + 16 * k) = ring[(((p0 >> 4) + k) & (R - 1)) * HONU_WAVE];
             nch = 0;
         }
@@ -462,7 +440,7 @@ HONU_DEV uint64_t encode_tail_bytes_noacl(const honu_meta &m, const uint32_t *__
     for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
         uint32_t r8[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? ((ENC_ABL & 4) ? 1000u * j : reg[ro + k0 + j]) : 0;
+        for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? reg[ro + k0 + j] : 0;
 #pragma unroll
         for (int j = 0; j < 8; j++) t += k0 + j < nr ? uvarint_len(r8[j]) : 0;
     }
@@ -557,7 +535,7 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
         for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
             uint32_t r8[8];
 #pragma unroll
-            for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? ((ENC_ABL & 4) ? 1000u * j : reg[ro + k0 + j]) : 0;
+            for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? reg[ro + k0 + j] : 0;
 #pragma unroll
             for (int j = 0; j < 8; j++) sfx += k0 + j < nr ? uvarint_len(r8[j]) : 0;
         }
@@ -576,8 +554,8 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
             const uint64_t T = (E & ~15ull) > hend ? (E & ~15ull) : hend;
             // the list's encoding at both ends (acl_chunk: 16 bytes from the
             // <= 2 entries they straddle), both loaded at once
-            const u32x4 hv = (ENC_ABL & 2) ? u32x4{1, 2, 3, 4} : acl_chunk(acl + ao, na, P, P);
-            const u32x4 tv = (ENC_ABL & 2) ? u32x4{5, 6, 7, 8} : E > T ? acl_chunk(acl + ao, na, P, T) : u32x4{0, 0, 0, 0};
+            const u32x4 hv = acl_chunk(acl + ao, na, P, P);
+            const u32x4 tv = E > T ? acl_chunk(acl + ao, na, P, T) : u32x4{0, 0, 0, 0};
             auto put_n = [&](const u32x4 &v, uint32_t cnt) {  // the first cnt (< 16) bytes of v
                 const uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
                 if (cnt >= 8) {
@@ -624,7 +602,7 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
     for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
         uint32_t r8[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? ((ENC_ABL & 4) ? 1000u * j : reg[ro + k0 + j]) : 0;
+        for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? reg[ro + k0 + j] : 0;
         W.drain();  // <= 15 + 10 before the first batch, <= 40 after one
 #pragma unroll
         for (int j = 0; j < 8; j++)
@@ -671,321 +649,5 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
     return acl_ret;
 }
 #undef OFF
-
-// ------------------------------------------------------------------------
-// The same encode with the record's inputs prefetched (ENC_PF): the loads a
-// record needs are issued in three batches whose addresses are known early -
-// (1) the row; (2) right after the header: the regions, the ACL entries the
-// list's two end chunks are built from, the Schema name and MIME bytes; (3) at
-// the Publisher: the IP, user agent, key, secret and the first 64 signature
-// bytes - each batch waited for once, instead of one round trip per frame
-// batch, region pass and ACL end (the encoder is latency bound,
-// ~22 dependent round trips per record). Bytes past a prefetch window (long
-// frames, more than 9 regions) are read as in encode_record_lane.
-// ------------------------------------------------------------------------
-// NB aligned 16-byte blocks from the start of a span (+ one zero word pad)
-template <int NB> struct PfBlocks {
-    uint64_t x[2 * NB + 2];
-    uint32_t a;  // the span's byte phase in x[0]
-    HONU_DEV void load(const uint8_t *base, uint64_t off, uint64_t len) {
-        const uint8_t *p = base + off;
-        a = (uint32_t)((uintptr_t)p & 15);
-        const u32x4 *w = reinterpret_cast<const u32x4 *>(p - a);
-        const uint64_t nw = len ? (a + len + 15) >> 4 : 0;
-#pragma unroll
-        for (int j = 0; j < NB; j++) {
-            u32x4 v{0, 0, 0, 0};
-            if ((uint64_t)j < nw) v = w[j];
-            x[2 * j] = ((uint64_t)v.y << 32) | v.x;
-            x[2 * j + 1] = ((uint64_t)v.w << 32) | v.z;
-        }
-        x[2 * NB] = x[2 * NB + 1] = 0;
-    }
-    // bytes of the span the blocks hold
-    HONU_DEV uint64_t held(uint64_t len) const {
-        const uint64_t c = 16ull * NB - a;
-        return len < c ? len : c;
-    }
-    // every loaded word in registers at this point (one wait for the batch)
-    HONU_DEV void pin() {
-#pragma unroll
-        for (int j = 0; j < 2 * NB; j++) asm volatile("" : "+v"(x[j]));
-    }
-};
-// the 10 words of ACL entries j0, j0 + 1 (zero past the list)
-struct AclPairW {
-    uint32_t w[10];
-    HONU_DEV void load(const honu_acl *A, uint64_t na, uint64_t j0) {
-#pragma unroll
-        for (int k = 0; k < 10; k++) w[k] = 0;
-        if (j0 < na) {
-            const uint32_t *e = reinterpret_cast<const uint32_t *>(A + j0);
-#pragma unroll
-            for (int k = 0; k < 5; k++) w[k] = e[k];
-        }
-        if (j0 + 1 < na) {
-            const uint32_t *e = reinterpret_cast<const uint32_t *>(A + j0 + 1);
-#pragma unroll
-            for (int k = 0; k < 5; k++) w[5 + k] = e[k];
-        }
-    }
-    HONU_DEV void pin() {
-#pragma unroll
-        for (int k = 0; k < 10; k++) asm volatile("" : "+v"(w[k]));
-    }
-    // acl_chunk(A, na, P, X) from the loaded entries (j0 = (X - P) / 18)
-    HONU_DEV u32x4 chunk(uint64_t na, uint64_t P, uint64_t X, uint64_t j0) const {
-        uint32_t b[10], d[5];
-        const uint32_t *e0 = w;
-        b[0] = 1u | (e0[0] << 8);
-        b[1] = (e0[0] >> 24) | (e0[1] << 8);
-        b[2] = (e0[1] >> 24) | (e0[2] << 8);
-        b[3] = (e0[2] >> 24) | (e0[3] << 8);
-        b[4] = (e0[3] >> 24) | ((e0[4] & 0xFF) << 8);
-        b[5] = b[6] = b[7] = b[8] = b[9] = 0;
-        if (j0 + 1 < na) {
-            const uint32_t *e1 = w + 5;
-            d[0] = 1u | (e1[0] << 8);
-            d[1] = (e1[0] >> 24) | (e1[1] << 8);
-            d[2] = (e1[1] >> 24) | (e1[2] << 8);
-            d[3] = (e1[2] >> 24) | (e1[3] << 8);
-            d[4] = (e1[3] >> 24) | ((e1[4] & 0xFF) << 8);
-            b[4] = (b[4] & 0xFFFF) | (d[0] << 16);
-            b[5] = (d[0] >> 16) | (d[1] << 16);
-            b[6] = (d[1] >> 16) | (d[2] << 16);
-            b[7] = (d[2] >> 16) | (d[3] << 16);
-            b[8] = (d[3] >> 16) | (d[4] << 16);
-        }
-        const uint32_t off = (uint32_t)(X - (P + 18 * j0));
-        const uint32_t q = off >> 2, sh = off & 3;
-        uint32_t o[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            uint32_t w0 = b[k], w1 = b[k + 1];
-#pragma unroll
-            for (int t = 1; t <= 4; t++)
-                if ((uint32_t)t == q) {
-                    w0 = b[t + k];
-                    w1 = b[t + k + 1];
-                }
-            o[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-        }
-        return u32x4{o[0], o[1], o[2], o[3]};
-    }
-};
-
-template <int R>
-HONU_DEV uint64_t encode_record_pf(const honu_meta &m, const uint8_t *__restrict__ var,
-                                   const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
-                                   uint64_t dlen, uint64_t beg, uint64_t end, uint8_t *__restrict__ out,
-                                   u32x4 *ring) {
-#define OFF(f) ((int)offsetof(honu_meta, f))
-    static_assert(R == 0 || R == 8, "drain spacing assumes 8 slots");
-    const uint8_t *mb = reinterpret_cast<const uint8_t *>(&m);
-    const uint32_t pr = m.present;
-    const uint64_t na = m.acl_count, ao = m.acl_off, nr = m.regions_count, ro = m.regions_off;
-    const bool has_schema = pr & HONU_HAS_SCHEMA, has_ver = pr & HONU_HAS_VERSION;
-    // positions from the row alone: tail start, ACL list start P, and the
-    // list's end if every entry is present (a nil entry is 1 byte, not 18)
-    const uint64_t t0 = beg + 1 + uvarint_len(dlen) + dlen;
-    uint64_t P = t0 + 1 + 32 + 1;
-    if (has_ver)
-        P += uvarint_len(m.pid) + uvarint_len(m.vid) + uvarint_len(m.region) + 1 +
-             ((pr & HONU_HAS_PARENT) ? uvarint_len(m.parent_pid) + uvarint_len(m.parent_vid) : 0) + 1 +
-             uvarint_len(zigzag(m.version_created));
-    P += 1;
-    if (has_schema)
-        P += frame_len(m.schema_name.len) + uvarint_len(m.schema_major) + uvarint_len(m.schema_minor) +
-             uvarint_len(m.schema_patch);
-    P += frame_len(m.mime.len) + 33 + uvarint_len(na);
-    const uint64_t Ef = P + 18 * na;  // the list's end if every entry is present
-    const uint64_t hend_f = ((P + 15) & ~15ull) < Ef ? ((P + 15) & ~15ull) : Ef;
-    const uint64_t Tf = (Ef & ~15ull) > hend_f ? (Ef & ~15ull) : hend_f;
-    // batch 2: regions, the ACL end entries, Schema name and MIME bytes
-    constexpr int NREG = 9;
-    uint32_t rg[NREG];
-#pragma unroll
-    for (int k = 0; k < NREG; k++) rg[k] = (uint64_t)k < nr ? reg[ro + k] : 0;
-    AclPairW ah, at;
-    ah.load(acl + ao, na, 0);
-    at.load(acl + ao, Ef > Tf ? na : 0, (Tf - P) / 18);
-    PfBlocks<3> fs, fm;
-    fs.load(var, m.schema_name.off, has_schema ? m.schema_name.len : 0);
-    fm.load(var, m.mime.off, m.mime.len);
-#pragma unroll
-    for (int k = 0; k < NREG; k++) asm volatile("" : "+v"(rg[k]));
-    ah.pin();
-    at.pin();
-    fs.pin();
-    fm.pin();
-    {  // header: version byte + uvarint(len data)   object.go:30,35
-        uint64_t lo, hi;
-        const uint32_t hn = uvarint_bytes(dlen, lo, hi);
-        out[beg] = HONU_STORAGE_VERSION;
-        for (uint32_t j = 0; j < hn; j++)
-            out[beg + 1 + j] = (uint8_t)(j < 8 ? lo >> (8 * j) : hi >> (8 * (j - 8)));
-    }
-    LaneWriterT<R> W;
-    W.init(out, t0);
-    W.set_ring(ring);
-    W.byte(1);                                                      // EncodeStruct(meta)
-    W.put16(ld64(mb + OFF(object_id)), ld64(mb + OFF(object_id) + 8));          // :110
-    W.put16(ld64(mb + OFF(collection_id)), ld64(mb + OFF(collection_id) + 8));  // :115
-    if (has_ver) {                                                  // :120, version.go:44-70
-        W.byte(1);
-        W.uv(m.pid);
-        W.uv(m.vid);
-        W.uv(m.region);
-        if (pr & HONU_HAS_PARENT) {
-            W.byte(1);
-            W.uv(m.parent_pid);
-            W.uv(m.parent_vid);
-        } else {
-            W.byte(0);
-        }
-        W.byte(m.tombstone ? 1 : 0);
-        W.uv(zigzag(m.version_created));
-    } else {
-        W.byte(0);
-    }
-    W.drain();  // <= 33 + 48 bytes since the last one
-    if (has_schema) {                                               // :125, schema.go:30-53
-        W.byte(1);
-        const uint64_t len = m.schema_name.len, k = fs.held(len);
-        W.uv(len);
-        W.put_words(fs.x, fs.a, k);
-        if (k < len) W.run(var + m.schema_name.off + k, len - k);
-        W.uv(m.schema_major);
-        W.uv(m.schema_minor);
-        W.uv(m.schema_patch);
-    } else {
-        W.byte(0);
-    }
-    W.drain();  // <= 1 + 10 + 48 + 15 (or a run's last batch + 15)
-    {                                                               // :130 MIME
-        const uint64_t len = m.mime.len, k = fm.held(len);
-        W.uv(len);
-        W.put_words(fm.x, fm.a, k);
-        if (k < len) W.run(var + m.mime.off + k, len - k);
-    }
-    W.drain();  // <= 58
-    W.put16(ld64(mb + OFF(owner)), ld64(mb + OFF(owner) + 8));      // :135
-    W.put16(ld64(mb + OFF(group)), ld64(mb + OFF(group) + 8));      // :140
-    W.byte(m.permissions);                                          // :145
-    W.uv(na);                                                       // :151
-    // the list is [P, E); E from the record's end and the fields after it
-    uint64_t sfx = uvarint_len(nr) + 3 + 1 + uvarint_len(zigzag(m.created)) + uvarint_len(zigzag(m.modified));
-#pragma unroll
-    for (int k = 0; k < NREG; k++) sfx += (uint64_t)k < nr ? uvarint_len(rg[k]) : 0;
-    for (uint64_t k = NREG; k < nr; k++) sfx += uvarint_len(reg[ro + k]);
-    if (pr & HONU_HAS_PUBLISHER) sfx += 32 + frame_len(m.ip_address.len) + frame_len(m.user_agent.len);
-    if (pr & HONU_HAS_ENCRYPTION)
-        sfx += frame_len(m.public_key_id.len) + frame_len(m.encryption_key.len) + frame_len(m.hmac_secret.len) +
-               frame_len(m.signature.len) + 3;
-    if (pr & HONU_HAS_COMPRESSION) sfx += 1 + uvarint_len(zigzag(m.compression_level));
-    const uint64_t E = end - sfx;
-    uint64_t acl_ret;
-    if (na && E == Ef) {
-        // every entry present: this lane writes the list's bytes in the
-        // partial 16-byte chunks at both ends (the group kernel the rest)
-        acl_ret = P | ACL_ALL_PRESENT;
-        const u32x4 hv = ah.chunk(na, P, P, 0);
-        const u32x4 tv = Ef > Tf ? at.chunk(na, P, Tf, (Tf - P) / 18) : u32x4{0, 0, 0, 0};
-        auto put_n = [&](const u32x4 &v, uint32_t cnt) {  // the first cnt (< 16) bytes of v
-            const uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
-            if (cnt >= 8) {
-                W.put(lo, 8);
-                if (cnt > 8) W.put(hi & ((1ull << (8 * (cnt - 8))) - 1), cnt - 8);
-            } else if (cnt) {
-                W.put(lo & ((1ull << (8 * cnt)) - 1), cnt);
-            }
-        };
-        put_n(hv, (uint32_t)(hend_f - P));  // <= 43 + 15 since the drain
-        if (Tf > hend_f) W.jump(Tf);
-        put_n(tv, (uint32_t)(Ef - Tf));
-    } else {
-        acl_ret = P;
-        W.jump(E);
-    }
-    W.uv(nr);                                                       // :164, region.go:137-152
-    W.drain();  // <= 15 + 10
-#pragma unroll
-    for (int k = 0; k < NREG; k++)
-        if ((uint64_t)k < nr) W.uv(rg[k]);  // <= 45 bytes
-    for (uint64_t k = NREG; k < nr; k++) {
-        if ((k - NREG) % 8 == 0) W.drain();
-        W.uv(reg[ro + k]);
-    }
-    W.drain();
-    // batch 3: every frame of the Publisher and the Encryption
-    const bool has_pub = pr & HONU_HAS_PUBLISHER, has_enc = pr & HONU_HAS_ENCRYPTION;
-    PfBlocks<3> fip, fua, fpk, fek, fhs;
-    PfBlocks<5> fsg;
-    fip.load(var, m.ip_address.off, has_pub ? m.ip_address.len : 0);
-    fua.load(var, m.user_agent.off, has_pub ? m.user_agent.len : 0);
-    fpk.load(var, m.public_key_id.off, has_enc ? m.public_key_id.len : 0);
-    fek.load(var, m.encryption_key.off, has_enc ? m.encryption_key.len : 0);
-    fhs.load(var, m.hmac_secret.off, has_enc ? m.hmac_secret.len : 0);
-    fsg.load(var, m.signature.off, has_enc ? m.signature.len : 0);
-    fip.pin();
-    fua.pin();
-    fpk.pin();
-    fek.pin();
-    fhs.pin();
-    fsg.pin();
-    auto frame_pf = [&](auto &B, const honu_span &sp) {
-        const uint64_t len = sp.len, k = B.held(len);
-        W.uv(len);
-        W.put_words(B.x, B.a, k);
-        if (k < len) W.run(var + sp.off + k, len - k);
-    };
-    if (has_pub) {                                                  // :169, provenance.go:34-57
-        W.byte(1);
-        W.put16(ld64(mb + OFF(publisher_id)), ld64(mb + OFF(publisher_id) + 8));
-        W.put16(ld64(mb + OFF(client_id)), ld64(mb + OFF(client_id) + 8));
-        W.drain();  // <= 33
-        frame_pf(fip, m.ip_address);
-        W.drain();  // <= 58 (or a run's last batch + 0)
-        frame_pf(fua, m.user_agent);
-    } else {
-        W.byte(0);
-    }
-    W.drain();  // <= 58
-    if (has_enc) {                                                  // :174, encryption.go:51-89
-        W.byte(1);
-        frame_pf(fpk, m.public_key_id);
-        W.drain();  // <= 59
-        frame_pf(fek, m.encryption_key);
-        W.drain();
-        frame_pf(fhs, m.hmac_secret);
-        W.drain();
-        {
-            const uint64_t len = m.signature.len, k = fsg.held(len);
-            W.uv(len);
-            W.put_words(fsg.x, fsg.a, k < 64 ? k : 64);  // <= 10 + 64 since the drain
-            if (len > 64) W.run(var + m.signature.off + 64, len - 64);  // run() drains first
-        }
-        W.byte(m.sealing_alg);
-        W.byte(m.encryption_alg);
-        W.byte(m.signature_alg);
-    } else {
-        W.byte(0);
-    }
-    W.drain();  // <= 64 + 3; then <= 12 + 1 + 20 to finish()
-    if (pr & HONU_HAS_COMPRESSION) {                                // :179, compression.go:40-53
-        W.byte(1);
-        W.byte(m.compression_alg);
-        W.uv(zigzag(m.compression_level));
-    } else {
-        W.byte(0);
-    }
-    W.byte(m.flags);                                                // :184
-    W.uv(zigzag(m.created));                                        // :189
-    W.uv(zigzag(m.modified));                                       // :194
-    W.finish();
-    return acl_ret;
-#undef OFF
-}
-
 
 }  // namespace honu

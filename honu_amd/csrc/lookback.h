@@ -189,6 +189,68 @@ HONU_DEV void lb_resolve_grouped(uint64_t *status, uint64_t *gstatus, uint64_t t
     }
 }
 
+// The grouped prefixes for ticket launches (tiles taken in order by running
+// waves, more tiles than waves): the group totals get a decoupled look-back of
+// their own. Tile words stay aggregates; group g's last tile publishes the
+// group total as soon as its group's aggregates are in (flag 1), and its
+// inclusive prefix through group g once it has its own prefix (flag 2). A tile
+// sums its group's earlier aggregates (one batch of loads) and looks back over
+// the group words, 64 groups (4,096 tiles) per round trip, to the nearest
+// inclusive one; groups resolve in ticket order, so that is one or two round
+// trips where the tile-level look-back took two or three.
+template <int K>
+HONU_DEV void lb_resolve_grouped_lb(uint64_t *status, uint64_t *gstatus, uint64_t t, uint64_t ntiles,
+                                    uint32_t ep, const uint64_t (&agg)[K], uint64_t (&excl)[K]) {
+    const uint32_t lane = lane_id();
+    const uint64_t g = t / HONU_WAVE, r = t % HONU_WAVE;
+    const bool closer = r == HONU_WAVE - 1 && t + 1 < ntiles;
+    uint32_t todo = (1u << K) - 1;              // bit c: this group's tiles before t
+    if (g) todo |= ((1u << K) - 1) << K;        // bit K + c: the groups before g
+    int64_t top[K];
+    uint64_t in_sum[K];
+#pragma unroll
+    for (int c = 0; c < K; c++) {
+        excl[c] = 0;
+        in_sum[c] = 0;
+        top[c] = (int64_t)g - 1;
+    }
+    for (;;) {
+#pragma unroll
+        for (int c = 0; c < 2 * K; c++) {
+            if (!(todo & (1u << c))) continue;
+            if (c < K) {
+                const uint64_t w = lane < r ? lb_load(status + (g * HONU_WAVE + lane) * K + c) : lb_word(1, ep, 0);
+                const bool ready = (w >> 62) != 0 && ((uint32_t)(w >> 44) & LB_EPOCH_MASK) == (ep & LB_EPOCH_MASK);
+                if (__ballot(!ready)) continue;
+                in_sum[c] = wave_sum(w & LB_VAL_MASK);
+                excl[c] += in_sum[c];
+                todo &= ~(1u << c);
+                if (closer && lane == 0) lb_store(gstatus + g * K + c, lb_word(1, ep, in_sum[c] + agg[c]));
+            } else {
+                const int col = c - K;
+                const int64_t idx = top[col] - (int64_t)lane;  // lane 0: the nearest group
+                const uint64_t w = idx >= 0 ? lb_load(gstatus + (uint64_t)idx * K + col) : lb_word(2, ep, 0);
+                const uint32_t fl = (uint32_t)(w >> 62);
+                const bool ready = fl != 0 && ((uint32_t)(w >> 44) & LB_EPOCH_MASK) == (ep & LB_EPOCH_MASK);
+                const uint64_t nb = __ballot(!ready), ib = __ballot(ready && fl == 2);
+                const uint32_t p = ib ? (uint32_t)__builtin_ctzll(ib) : 64;
+                const uint64_t upto = p >= 63 ? ~0ull : ((2ull << p) - 1);
+                if (nb & upto) continue;
+                excl[col] += wave_sum(lane <= p ? (w & LB_VAL_MASK) : 0);
+                if (p < 64) todo &= ~(1u << c);
+                else top[col] -= 64;
+            }
+        }
+        if (!todo) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if (closer) {  // the group's inclusive prefix: this tile's own inclusive one
+#pragma unroll
+        for (int c = 0; c < K; c++)
+            if (lane == (uint32_t)c) lb_store(gstatus + g * K + c, lb_word(2, ep, excl[c] + agg[c]));
+    }
+}
+
 // The scans' end (scan.hip; the single-launch decode ends in lb_finish_blocks).
 // Called by every wave with the ticket that ended its loop (t_end >= ntiles):
 // a wave takes that ticket only after finishing its last tile, so the wave
