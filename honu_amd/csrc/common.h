@@ -216,40 +216,10 @@ HONU_DEV void wave_copy_bytes(uint8_t *__restrict__ dst, const uint8_t *__restri
 // page, so the over-read is always mapped.
 // NT: non-temporal cache policy, 0 none, 1 loads and stores, 2 loads only,
 // 3 stores only; 4: a misaligned source is read with one unaligned 16-byte
-// load per chunk instead of two aligned loads and a funnel; 5 (A/B): one
-// aligned load per chunk, the funnel's second block taken from the next lane
-// by a DPP wave shift (wave_shl:1) - lane 63's from lane 0 of the next
-// unrolled row - and loaded directly only by the last chunk's lane and by
-// lane 63 of the last row: a third fewer load requests through the L1 (the
-// copies run with TA / TD 91-98 % busy, DESIGN §3 "Round 4").
+// load per chunk instead of two aligned loads and a funnel.
 // The head bytes, the tail bytes and the first UNROLL x 64 chunks are all
 // loaded before any of them is stored, so a short segment (the common case
 // for Small records: 2.5 KB) costs one round trip, not three.
-// wave_copy NT 5: b[u] (the aligned source block after this lane's chunk)
-// from the next lane's a[u] by a DPP wave shift; lanes that loaded b
-// themselves (own) keep it. All lanes call it (converged).
-template <int UNROLL>
-HONU_DEV void dpp_second(const u32x4 (&a)[UNROLL], u32x4 (&b)[UNROLL], uint64_t c, uint64_t chunks) {
-    const uint32_t lane = lane_id();
-#pragma unroll
-    for (int u = 0; u < UNROLL; u++) {
-        u32x4 v;
-        v.x = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[u].x, 0x130, 0xF, 0xF, true);  // wave_shl:1
-        v.y = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[u].y, 0x130, 0xF, 0xF, true);
-        v.z = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[u].z, 0x130, 0xF, 0xF, true);
-        v.w = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[u].w, 0x130, 0xF, 0xF, true);
-        if (u + 1 < UNROLL) {  // lane 63: lane 0's block of the next row
-            const u32x4 &nx = a[u + 1 < UNROLL ? u + 1 : u];
-            const uint32_t x0 = __builtin_amdgcn_readlane(nx.x, 0), x1 = __builtin_amdgcn_readlane(nx.y, 0);
-            const uint32_t x2 = __builtin_amdgcn_readlane(nx.z, 0), x3 = __builtin_amdgcn_readlane(nx.w, 0);
-            if (lane == HONU_WAVE - 1) v = u32x4{x0, x1, x2, x3};
-        }
-        const uint64_t cu = c + (uint64_t)u * HONU_WAVE;
-        const bool own = cu + 1 >= chunks || (lane == HONU_WAVE - 1 && u == UNROLL - 1);
-        if (cu < chunks && !own) b[u] = v;
-    }
-}
-
 template <int UNROLL = 4, int NT = 0>
 HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint64_t n) {
     if (n == 0) return;
@@ -264,12 +234,7 @@ HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ s
     const uint8_t *bsrc = src + head;
     const uint32_t p = (uint32_t)((uint64_t)bsrc & 15u);  // wave-uniform
     const u32x4 *__restrict__ s4 = reinterpret_cast<const u32x4 *>(bsrc - p);
-    auto load = [&](uint64_t c, u32x4 &a, u32x4 &b, int u) {
-        if (NT == 5) {  // the second block only where no neighbour lane holds it
-            a = *(&s4[c]);
-            if (p && (c + 1 >= chunks || (lane == HONU_WAVE - 1 && u == UNROLL - 1))) b = s4[c + 1];
-            return;
-        }
+    auto load = [&](uint64_t c, u32x4 &a, u32x4 &b) {
         if (NT == 4 && p) {
             a = *reinterpret_cast<const u32x4u *>(bsrc + 16 * c);
         } else {
@@ -288,9 +253,7 @@ HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ s
         u32x4 a[UNROLL], b[UNROLL];
 #pragma unroll
         for (int u = 0; u < UNROLL; u++)
-            if (lane + u * HONU_WAVE < chunks) load(lane + u * HONU_WAVE, a[u], b[u], u);
-        if constexpr (NT == 5)
-            if (p) dpp_second(a, b, (uint64_t)lane, chunks);
+            if (lane + u * HONU_WAVE < chunks) load(lane + u * HONU_WAVE, a[u], b[u]);
         if (lane < head) dst[lane] = hv;
 #pragma unroll
         for (int u = 0; u < UNROLL; u++)
@@ -303,9 +266,7 @@ HONU_DEV void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ s
         u32x4 a[UNROLL], b[UNROLL];
 #pragma unroll
         for (int u = 0; u < UNROLL; u++)
-            if (c + u * HONU_WAVE < chunks) load(c + u * HONU_WAVE, a[u], b[u], u);
-        if constexpr (NT == 5)
-            if (p) dpp_second(a, b, c, chunks);
+            if (c + u * HONU_WAVE < chunks) load(c + u * HONU_WAVE, a[u], b[u]);
 #pragma unroll
         for (int u = 0; u < UNROLL; u++)
             if (c + u * HONU_WAVE < chunks) store(c + u * HONU_WAVE, a[u], b[u]);

@@ -212,8 +212,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_sweep(Seg seg, uint64_t n,
 // Copy-engine variants (A/B build only, tools/tune_copy.py): 1-5 contiguous
 // per-wave ranges {unroll, non-temporal}; 6-7 the sweep form; 11 / 12
 // non-temporal loads only / stores only; 13-15 one unaligned 16-byte load per
-// chunk instead of two aligned loads and a funnel; 16 the funnel's second
-// block by a DPP wave shift (wave_copy NT 5). The product library has
+// chunk instead of two aligned loads and a funnel. The product library has
 // variant 0 only (unroll 4, default cache policy: measured fastest).
 template <class Seg>
 static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
@@ -241,7 +240,6 @@ static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
     case 13: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 4>), grid, block, 0, s, seg, n, total); return hipGetLastError();
     case 14: hipLaunchKernelGGL((k_copy_segments<Seg, 8, 4>), grid, block, 0, s, seg, n, total); return hipGetLastError();
     case 15: hipLaunchKernelGGL((k_copy_segments<Seg, 2, 4>), grid, block, 0, s, seg, n, total); return hipGetLastError();
-    case 16: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 5>), grid, block, 0, s, seg, n, total); return hipGetLastError();
     default: break;
     }
 #endif

@@ -297,8 +297,7 @@ def test_long_tails_and_nil_entries_parity(codec, oracle_lib):
 
 
 @pytest.mark.parametrize("lens", ["tiny", "edges", "skew"])
-@pytest.mark.parametrize("copy_variant", [0, 1, 6, 11, 12, 13, 16],
-                         ids=["default", "unroll8", "sweep", "nt_load", "nt_store", "unaligned", "dpp"])
+@pytest.mark.parametrize("copy_variant", [0, 1, 6, 11, 12, 13], ids=["default", "unroll8", "sweep", "nt_load", "nt_store", "unaligned"])
 def test_copy_engine_parity(oracle_lib, copy_variant, lens):
     """The payload copy engine on awkward length mixes: payloads of 0-40 bytes
     (head/tail bytes only), lengths around multiples of 16, and a skewed mix of
