@@ -66,12 +66,21 @@ constexpr uint64_t FUSED_SPEC_MIN_TILES = 768;
 #endif
 constexpr uint32_t STAGE_SLOTS = STAGE_SLOTS_N;
 static_assert(STAGE_SLOTS % HONU_WAVE == 0, "whole instructions");
-// a wave's LDS: its windows during the walk, the staging after it (two
-// 4-wave workgroups per CU still fit the 160 KB)
-constexpr uint32_t FUSED_WAVE_BYTES =
-    STAGE_SLOTS * 16 + 32 > WIN_WAVE_BYTES ? STAGE_SLOTS * 16 + 32 : WIN_WAVE_BYTES;
-static_assert(2 * HONU_WAVES_PER_BLOCK * FUSED_WAVE_BYTES + 64 <= 160 * 1024, "2 workgroups per CU");
+// Launch forms: FORM_TICKET (more tiles than resident waves), FORM_STATIC
+// (every tile a resident wave). (A third form for launches that need at most
+// one workgroup per CU, with twice the staging area so a tile's lists stage in
+// one round issued before the look-back wait, measured equal: 62 K Large
+// 0.081-0.085 vs 0.082-0.084 ms, 64 K XLarge 0.0735 vs 0.0732 ms,
+// profiles/r04/ab/wide_static_ab.jsonl.)
+enum { FORM_TICKET = 0, FORM_STATIC = 1 };
+template <int FORM> constexpr uint32_t form_slots() { return STAGE_SLOTS; }
+// a wave's LDS: its windows during the walk, the staging after it
+template <int FORM> constexpr uint32_t form_wave_bytes() {
+    return form_slots<FORM>() * 16 + 32 > WIN_WAVE_BYTES ? form_slots<FORM>() * 16 + 32 : WIN_WAVE_BYTES;
+}
+static_assert(2 * HONU_WAVES_PER_BLOCK * form_wave_bytes<FORM_STATIC>() + 64 <= 160 * 1024, "2 workgroups per CU");
 
+template <uint32_t SLOTS>
 struct AclStage {
     uint64_t apos;   // this lane's first flag
     uint32_t nb, B;  // this lane's blocks, exclusive prefix over the wave
@@ -82,7 +91,7 @@ struct AclStage {
     HONU_DEV void init(bool fl, uint64_t apos_, uint64_t nacl_) {
         apos = apos_;
         const uint64_t b = fl ? ((apos + 18 * nacl_ + 15) >> 4) - (apos >> 4) : 0;
-        const bool st = b && b <= STAGE_SLOTS;
+        const bool st = b && b <= SLOTS;
         nb = st ? (uint32_t)b : 0;
         nacl = st ? (uint32_t)nacl_ : 0;
         B = wave_excl32(nb, nbtot);
@@ -92,10 +101,10 @@ struct AclStage {
     }
     HONU_DEV bool staged() const { return nacl != 0; }
     HONU_DEV bool more() const { return start < nbtot; }
-    // the round: lanes [r0, r1) whose blocks end within start + STAGE_SLOTS
+    // the round: lanes [r0, r1) whose blocks end within start + SLOTS
     // (B + nb is non-decreasing over the lanes)
     HONU_DEV void plan() {
-        const uint64_t m = __ballot(B + nb <= start + STAGE_SLOTS);
+        const uint64_t m = __ballot(B + nb <= start + SLOTS);
         r1 = (uint32_t)__builtin_popcountll(m);
         stop = r1 < HONU_WAVE ? __builtin_amdgcn_readlane(B, r1) : nbtot;
     }
@@ -111,7 +120,7 @@ struct AclStage {
     HONU_DEV void issue(uint8_t *ws, const uint8_t *__restrict__ rec) const {
         const uint32_t lane = lane_id();
 #pragma unroll
-        for (uint32_t k = 0; k < STAGE_SLOTS / HONU_WAVE; k++) {
+        for (uint32_t k = 0; k < SLOTS / HONU_WAVE; k++) {
             const uint32_t w0 = start + HONU_WAVE * k;
             if (w0 >= stop) break;  // wave-uniform
             const uint32_t r = (uint32_t)__builtin_popcountll(__ballot(B <= w0)) - 1;
@@ -230,21 +239,24 @@ struct SpecPub {
 
 // MODE 0: plain; 1: speculative publish; 2: guarded recovery (runs only when
 // the speculative launch before it raised misspec). Three instantiations, so
-// profiles tell the launches apart. STAT: every tile has a resident wave of
-// its own (tiles <= waves, known at launch): static tiles and grouped prefixes
-// instead of tickets and the decoupled look-back (lookback.h); a kernel of its
-// own, so neither form pays the other's registers.
-template <int MODE, bool STAT>
+// profiles tell the launches apart. FORM (FORM_*, chosen at launch): static
+// forms give every tile a resident wave of its own (tiles <= waves): static
+// tiles and grouped prefixes instead of tickets and the look-back over group
+// totals (lookback.h); each form a kernel of its own, so none pays another's
+// registers or LDS.
+template <int MODE, int FORM>
 __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
     DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t *lb_gstatus, uint64_t lb_words) {
     constexpr int mode = MODE;
     if (mode == 2 && __hip_atomic_load(&lb->misspec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
         return;  // every wave of the launch returns: the look-back state is untouched
-    __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * FUSED_WAVE_BYTES];
+    constexpr bool STAT = FORM != FORM_TICKET;
+    constexpr uint32_t WAVE_BYTES = form_wave_bytes<FORM>();
+    __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * WAVE_BYTES];
     __shared__ uint32_t last_flag;
     __shared__ uint32_t wg_ticket;
-    uint8_t *ws = smem + (threadIdx.x / HONU_WAVE) * FUSED_WAVE_BYTES;
+    uint8_t *ws = smem + (threadIdx.x / HONU_WAVE) * WAVE_BYTES;
     const uint32_t lane = lane_id();
     const uint32_t ep = lb_epoch(lb);
     const uint64_t ntiles = (n + HONU_WAVE - 1) / HONU_WAVE;
@@ -327,7 +339,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         // first round of their blocks is staged now, before the wait, as it
         // needs no offsets
         const bool fl = valid && P.st == HONU_OK && P.nacl && (P.acl_pos & GRP_ACL_FAST);
-        AclStage S;
+        AclStage<form_slots<FORM>()> S;
         S.init(fl, P.acl_pos & GRP_POS_MASK, P.nacl);
         if (S.more()) S.issue(ws, rec);
         WSTAMP(10);  // publish + rows out + first staging round issued
@@ -487,10 +499,10 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
     const dim3 grid((unsigned)b), block(HONU_BLOCK);
 #define HONU_FUSED_LAUNCH(M)                                                                               \
     do {                                                                                                   \
-        if (stat) hipLaunchKernelGGL((k_decode_fused<M, true>), grid, block, 0, s, rec, rec_off, n, O, lb,  \
-                                     lb_status, lb_gstatus, lb_words);                                                 \
-        else hipLaunchKernelGGL((k_decode_fused<M, false>), grid, block, 0, s, rec, rec_off, n, O, lb,      \
-                                lb_status, lb_gstatus, lb_words);                                                      \
+        if (stat) hipLaunchKernelGGL((k_decode_fused<M, FORM_STATIC>), grid, block, 0, s, rec, rec_off, n,  \
+                                     O, lb, lb_status, lb_gstatus, lb_words);                              \
+        else hipLaunchKernelGGL((k_decode_fused<M, FORM_TICKET>), grid, block, 0, s, rec, rec_off, n, O,   \
+                                lb, lb_status, lb_gstatus, lb_words);                                      \
     } while (0)
     if (tiles < FUSED_SPEC_MIN_TILES) {
         HONU_FUSED_LAUNCH(0);

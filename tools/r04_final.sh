@@ -35,6 +35,8 @@ if [ "$part" = 1 ]; then
     > $out/traffic_large.txt || exit 7
 fi
 if [ "$part" = 2 ]; then
+  tools/pmc_passes.sh $out/pmc_large2 "TA_TA_BUSY_sum TD_TD_BUSY_sum TCP_PENDING_STALL_CYCLES_sum GRBM_GUI_ACTIVE" \
+    -- python3 bench.py --no-cpu-baseline --no-host-path --no-decode-legs > $out/pmc_large2.log 2>&1 || exit 4
   tools/pmc_passes.sh $out/pmc_zc "FETCH_SIZE" "WRITE_SIZE" \
     -- python3 bench.py --mode decode --decode-leg zero_copy --no-cpu-baseline --no-host-path > $out/pmc_zc.log 2>&1 || exit 1
   timeout -k 10 400 python bench.py --mode decode --decode-leg zero_copy --no-cpu-baseline --no-host-path \
