@@ -36,15 +36,16 @@ def _gpu():
 
 
 @pytest.mark.parametrize("decode", ["fused", "split"])
-@pytest.mark.parametrize("after,beside", [("scan", "encode"), ("meta", "encode"), ("scan", "decode")])
+@pytest.mark.parametrize("after,beside,ms", [("scan", "encode", 1), ("meta", "encode", 1), ("scan", "decode", 1),
+                                             ("scan", "encode", 2)])
 @pytest.mark.parametrize("shape,n", [("small", 4000), ("mixed", 1200), ("large", 160)])
-def test_bench_pipeline_bit_exact(oracle_lib, shape, n, after, decode, beside):
+def test_bench_pipeline_bit_exact(oracle_lib, shape, n, after, decode, beside, ms):
     seed = 7
     args = bench.parse_args(["--records", str(n), "--shape", shape, "--min-chunks", "5",
                              "--encode-copy-after", after, "--seed", str(seed),
-                             "--decode", decode, "--meta-beside", beside])
+                             "--decode", decode, "--meta-beside", beside, "--meta-streams", str(ms)])
     b = bench.Bench(args, 0, 0)
-    assert len(b.chunks) >= 5 and len(b.slots) == 2
+    assert len(b.chunks) >= 5 and len(b.slots) == 2 and len(b.sms) == ms
     hb = gen_host_batch(seed, shape, 0, n)  # the same records the device generator made
     seen = []
 
