@@ -12,16 +12,20 @@ namespace honu {
 // ------------------------------------------------------------------------
 // encode: header + Metadata tail (object.go:24-45, metadata.go:108-200)
 // ------------------------------------------------------------------------
-#ifndef ENC_RING
-#define ENC_RING 8  // chunks in the writer's LDS ring per lane (0: direct stores)
-#endif
+// The ring: RING 16-byte chunks per lane, slot-major with the wave's lanes
+// adjacent (ring slot k of lane L at area + 16 (64 k + L)). Two forms, chosen
+// at launch: RING 8 (drains of every full chunk; 32 KB of LDS per workgroup,
+// the registers allow 3 waves per SIMD) where a launch has at most as many
+// tiles as the line form has resident waves, RING 16 (line drains, lane.h;
+// 64 KB per workgroup: 2 waves per SIMD) above that. Measured (interleaved,
+// profiles/r04/ab/enc_line_drain_ab.jsonl): 1M Small 1.09 -> 0.99 ms, 262 K
+// Small 0.298 -> 0.265 ms; 64 K Small 0.074 -> 0.078 ms and a 62 K Large chunk
+// 0.082 -> 0.086 ms (latency-bound: fewer records in flight per SIMD and
+// lines held back lengthen a tile), hence the switch.
+constexpr uint64_t ENC_LINE_MIN_TILES = 2 * 4 * 256;  // the line form's resident waves (2 workgroups x 4 waves x 256 CUs)
+template <int RING> constexpr uint32_t enc_wave_bytes() { return (RING > 0 ? RING : 1) * HONU_WAVE * 16; }
 
-
-// The ring: ENC_RING 16-byte chunks per lane, slot-major with the wave's
-// lanes adjacent (ring slot k of lane L at area + 16 (64 k + L)).
-constexpr uint32_t ENC_WAVE_BYTES = (ENC_RING > 0 ? ENC_RING : 1) * HONU_WAVE * 16;
-
-template <bool SKIP_ACL>
+template <bool SKIP_ACL, int RING>
 HONU_DEV void k_encode_meta_lane_one(uint64_t i, const honu_meta &m, const uint8_t *__restrict__ var,
     const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
     const uint64_t *__restrict__ payload_off, uint8_t *__restrict__ out,
@@ -34,8 +38,8 @@ HONU_DEV void k_encode_meta_lane_one(uint64_t i, const honu_meta &m, const uint8
         return;
     }
     const uint64_t dlen = payload_off[i + 1] - payload_off[i];
-    const uint64_t pos = encode_record_lane<SKIP_ACL, SKIP_ACL ? ENC_RING : 0>(m, var, acl, reg, dlen, beg, end,
-                                                                           out, ring);
+    const uint64_t pos = encode_record_lane<SKIP_ACL, SKIP_ACL ? RING : 0>(m, var, acl, reg, dlen, beg, end,
+                                                                       out, ring);
     if constexpr (SKIP_ACL) acl_out[i] = pos;
 }
 
@@ -48,15 +52,16 @@ HONU_DEV void load_row(const honu_meta *__restrict__ src, honu_meta &m) {
     for (int k = 0; k < 22; k++) d[k] = s[k];
 }
 
-template <bool SKIP_ACL>
+template <bool SKIP_ACL, int RING>
 __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
     const honu_meta *__restrict__ meta, const uint8_t *__restrict__ var,
     const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
     const uint64_t *__restrict__ payload_off, uint64_t n, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status,
     uint64_t *__restrict__ acl_out) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * ENC_WAVE_BYTES];
-    uint8_t *area = smem + (threadIdx.x / HONU_WAVE) * ENC_WAVE_BYTES;
+    constexpr uint32_t WAVE_BYTES = enc_wave_bytes<RING>();
+    __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * WAVE_BYTES];
+    uint8_t *area = smem + (threadIdx.x / HONU_WAVE) * WAVE_BYTES;
     u32x4 *ring = reinterpret_cast<u32x4 *>(area) + lane_id();
     // wave-uniform loop over tiles of 64 records (one per lane)
     for (uint64_t t0 = (uint64_t)blockIdx.x * HONU_BLOCK + (threadIdx.x & ~(uint64_t)(HONU_WAVE - 1)); t0 < n;
@@ -66,7 +71,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
         honu_meta m;
         if (i < n) {
             load_row(meta + i, m);
-            k_encode_meta_lane_one<SKIP_ACL>(i, m, var, acl, reg, payload_off, out, out_cap, out_off, status,
+            k_encode_meta_lane_one<SKIP_ACL, RING>(i, m, var, acl, reg, payload_off, out, out_cap, out_off, status,
                                              acl_out, ring);
         }
     }
@@ -192,8 +197,12 @@ hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, co
                                    int32_t *status, uint64_t *acl_out, int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (!acl_out) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_encode_meta_lane<true>, lane_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta, var,
-                       acl, reg, payload_off, n, out, out_cap, out_off, status, acl_out);
+    if ((n + HONU_WAVE - 1) / HONU_WAVE > ENC_LINE_MIN_TILES)
+        hipLaunchKernelGGL((k_encode_meta_lane<true, 16>), lane_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta,
+                           var, acl, reg, payload_off, n, out, out_cap, out_off, status, acl_out);
+    else
+        hipLaunchKernelGGL((k_encode_meta_lane<true, 8>), lane_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta,
+                           var, acl, reg, payload_off, n, out, out_cap, out_off, status, acl_out);
     return hipGetLastError();
 }
 
