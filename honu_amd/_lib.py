@@ -33,6 +33,7 @@ _PROTOS = {
     "honu_ctx_destroy": (None, [P]),
     "honu_ctx_max_records": (U64, [P]),
     "honu_ctx_set_param": (I32, [P, C.c_char_p, C.c_int64]),
+    "honu_ctx_get_param": (I32, [P, C.c_char_p, P]),
     "honu_ctx_reset": (I32, [P, P]),
     "honu_encode_sizes": (I32, [P, P, U64, P, U64, P, U64, P, U64, P, P, P]),
     "honu_exclusive_scan": (I32, [P, P, U64, P, P]),

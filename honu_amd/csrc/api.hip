@@ -31,7 +31,15 @@ struct honu_ctx {
     uint64_t lb_dec_words;     // tile + group words
     uint64_t lb_bytes;       // the look-back blocks + status words, from lb_dec
     ScanState scan;          // look-back state of the one-launch scans (scan.hip)
+    // speculation back-off (fused.hip): a guarded recovery launch that ran sets
+    // *spec_seen (pinned host word, written by the device); the next call sees
+    // it and decodes SPEC_BACKOFF_CALLS calls without speculation, so a stream
+    // of batches with malformed records pays ~1.1x instead of ~2x per batch
+    uint32_t *spec_seen;
+    uint32_t spec_off;       // calls left without speculation
+    bool spec_allowed;       // honu_ctx_set_param("speculate", 0) turns it off
 };
+static constexpr uint32_t SPEC_BACKOFF_CALLS = 16;
 
 static thread_local char g_last_error[256];
 
@@ -160,6 +168,16 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
         *err = HONU_E_HIP;
         return nullptr;
     }
+    if (hipHostMalloc((void **)&c->spec_seen, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+        hipSuccess) {
+        snprintf(g_last_error, sizeof g_last_error, "hipHostMalloc(spec_seen) failed");
+        (void)hipFree(c->ws);
+        free(c);
+        *err = HONU_E_HIP;
+        return nullptr;
+    }
+    *c->spec_seen = 0;
+    c->spec_allowed = true;
     uint64_t *w = (uint64_t *)c->ws;
     c->counts = w;
     w += 3 * n;
@@ -190,6 +208,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     if (s) (void)hipStreamDestroy(s);
     if (!ok) {
         (void)hipFree(c->ws);
+        (void)hipHostFree(c->spec_seen);
         free(c);
         *err = HONU_E_HIP;
         return nullptr;
@@ -209,6 +228,7 @@ void honu_ctx_destroy(honu_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipFree(ctx->ws);
+    (void)hipHostFree(ctx->spec_seen);
     free(ctx);
 }
 
@@ -219,6 +239,7 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
     if (!strcmp(name, "copy_blocks") && value > 0) ctx->geom.copy_blocks = (int)value;
     else if (!strcmp(name, "record_blocks") && value > 0) ctx->geom.per_record_blocks = (int)value;
     else if (!strcmp(name, "lane_blocks") && value >= 0) ctx->geom.lane_blocks = (int)value;
+    else if (!strcmp(name, "speculate") && (value == 0 || value == 1)) ctx->spec_allowed = value != 0;
     else if (!strcmp(name, "copy_variant") && value >= 0 && (value == 0 || HONU_AB_BUILD))
         ctx->geom.copy_variant = (int)value;
     else if (!strcmp(name, "encode_variant") && (value == 0 || value == 1))
@@ -226,6 +247,21 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
     else if (!strcmp(name, "record_variant") &&
              (value == 0 || value == 5 || value == 6))
         ctx->geom.record_variant = (int)value;
+    else return arg_fail(name);
+    return HONU_OK;
+}
+
+int32_t honu_ctx_get_param(const honu_ctx *ctx, const char *name, int64_t *value) {
+    if (!ctx || !name || !value) return arg_fail("ctx/name/value");
+    if (!strcmp(name, "copy_blocks")) *value = ctx->geom.copy_blocks;
+    else if (!strcmp(name, "record_blocks")) *value = ctx->geom.per_record_blocks;
+    else if (!strcmp(name, "lane_blocks")) *value = ctx->geom.lane_blocks;
+    else if (!strcmp(name, "speculate")) *value = ctx->spec_allowed ? 1 : 0;
+    else if (!strcmp(name, "speculate_backoff"))  // calls the next call starts without speculation
+        *value = __atomic_load_n(ctx->spec_seen, __ATOMIC_RELAXED) ? SPEC_BACKOFF_CALLS : ctx->spec_off;
+    else if (!strcmp(name, "copy_variant")) *value = ctx->geom.copy_variant;
+    else if (!strcmp(name, "encode_variant")) *value = ctx->geom.encode_variant;
+    else if (!strcmp(name, "record_variant")) *value = ctx->geom.record_variant;
     else return arg_fail(name);
     return HONU_OK;
 }
@@ -407,10 +443,18 @@ int32_t honu_decode_records(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t 
         HIPCHK(hipMemsetAsync(tot, 0, 3 * sizeof(uint64_t), s));
         return HONU_OK;
     }
+    // speculation back-off: a recovery of an earlier call has finished (the
+    // word is read without waiting: a recovery still in flight is seen later)
+    if (__atomic_load_n(ctx->spec_seen, __ATOMIC_RELAXED)) {
+        __atomic_store_n(ctx->spec_seen, 0u, __ATOMIC_RELAXED);
+        ctx->spec_off = SPEC_BACKOFF_CALLS;
+    }
+    const bool spec = ctx->spec_allowed && ctx->spec_off == 0;
+    if (ctx->spec_off) ctx->spec_off--;
     HIPCHK(launch_decode_fused(d_rec, d_rec_off, n, d_meta, d_info, d_acl, acl_cap, d_regions,
                                regions_cap, materialize != 0, data_cap, ctx->scratch, ctx->offs,
                                tot, ctx->lb_dec, ctx->lb_dec_status, ctx->lb_dec_gstatus,
-                               ctx->lb_dec_words, fused_blocks(ctx->geom), s));
+                               ctx->lb_dec_words, fused_blocks(ctx->geom), ctx->spec_seen, spec, s));
     return HONU_OK;
 }
 

@@ -150,13 +150,20 @@ struct AclStage {
     // returns true when an entry flag of the round is not 1 (checked only
     // with chk: the walk speculated that every entry is present)
     // (an entry is five aligned dword LDS reads and four v_alignbyte: 1M Small
-    // 0.760 -> 0.747 ms against two 16-byte reads and window16's select chain)
+    // 0.760 -> 0.747 ms against two 16-byte reads and window16's select chain.
+    // Round 4, measured and not kept: two or four entries per lane per pass,
+    // one list walk per pass (equal); and as measurement-only builds, the
+    // table stores left out (1M Small 0.708 -> 0.560 ms, 62 K Large 0.082 ->
+    // 0.072 ms) or the same bytes as contiguous 16-byte stores (0.693 ms,
+    // 0.079 ms): the table's bytes, not the store pattern, are the cost.
+    // profiles/r04/ab/dec_fill_*.jsonl)
     template <class AfterWait>
     HONU_DEV bool store(const uint8_t *ws, honu_acl *__restrict__ acl, uint64_t ao, bool ok,
                         bool chk, AfterWait after_wait) const {
         const uint32_t lane = lane_id();
         __builtin_amdgcn_s_waitcnt(0);  // the round's blocks have landed
         wave_sync();
+        WSTAMP(14);  // fill: the round's wait (its DMA, and every store before it)
         after_wait();
         const bool in = lane >= r0 && lane < r1;
         uint32_t etot;
@@ -207,6 +214,7 @@ struct AclStage {
                 d[4] = pm | (1u << 8);
             }
         }
+        WSTAMP(15);  // fill: the round's passes
         wave_sync();  // the LDS is the next round's (or the next tile's windows)
         return bad;
     }
@@ -247,10 +255,15 @@ struct SpecPub {
 template <int MODE, int FORM>
 __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
-    DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t *lb_gstatus, uint64_t lb_words) {
+    DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t *lb_gstatus, uint64_t lb_words,
+    uint32_t *spec_seen) {
     constexpr int mode = MODE;
     if (mode == 2 && __hip_atomic_load(&lb->misspec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
         return;  // every wave of the launch returns: the look-back state is untouched
+    // a recovery that runs tells the host (the context's pinned word), which
+    // then decodes the context's next calls without speculation (api.hip)
+    if (mode == 2 && spec_seen && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(spec_seen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     constexpr bool STAT = FORM != FORM_TICKET;
     constexpr uint32_t WAVE_BYTES = form_wave_bytes<FORM>();
     __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * WAVE_BYTES];
@@ -458,6 +471,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
             __hip_atomic_store(&lb->misspec, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         WSTAMP(13);  // ACL fill
     }
+    WSTAMP_FLUSH();
     lb_finish_blocks(lb, lb_status, lb_words, gridDim.x, &last_flag, mode == 2);
 }
 
@@ -480,7 +494,8 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
                                uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap, int materialize,
                                uint64_t data_cap, DecodeScratch *scratch, uint64_t *offs,
                                uint64_t *totals, LbState *lb, uint64_t *lb_status,
-                               uint64_t *lb_gstatus, uint64_t lb_words, int max_blocks, hipStream_t s) {
+                               uint64_t *lb_gstatus, uint64_t lb_words, int max_blocks, uint32_t *spec_seen,
+                               bool allow_spec, hipStream_t s) {
     if (n == 0) return hipSuccess;
     // (32-record tiles for batches whose 64-record tiles fill at most half the
     // resident waves, so that every SIMD walks records, measured slower with
@@ -500,11 +515,11 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
 #define HONU_FUSED_LAUNCH(M)                                                                               \
     do {                                                                                                   \
         if (stat) hipLaunchKernelGGL((k_decode_fused<M, FORM_STATIC>), grid, block, 0, s, rec, rec_off, n,  \
-                                     O, lb, lb_status, lb_gstatus, lb_words);                              \
+                                     O, lb, lb_status, lb_gstatus, lb_words, spec_seen);                   \
         else hipLaunchKernelGGL((k_decode_fused<M, FORM_TICKET>), grid, block, 0, s, rec, rec_off, n, O,   \
-                                lb, lb_status, lb_gstatus, lb_words);                                      \
+                                lb, lb_status, lb_gstatus, lb_words, spec_seen);                           \
     } while (0)
-    if (tiles < FUSED_SPEC_MIN_TILES) {
+    if (tiles < FUSED_SPEC_MIN_TILES || !allow_spec) {
         HONU_FUSED_LAUNCH(0);
         return hipGetLastError();
     }

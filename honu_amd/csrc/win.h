@@ -204,24 +204,39 @@ static __device__ uint64_t g_walk_stamps[1 << 16][WALK_STAMPS];  // per translat
 // Timing build only (-DHONU_STAGE_TIMING, tools/fused_timing.py): lane 0 of
 // every wave ADDS the time since its previous stamp to stage k, over every tile
 // the wave takes, so the sums divided by the tiles give the stage costs under
-// full load (the single-launch decode stamps its post-walk stages as 10..13).
+// full load (the single-launch decode stamps its post-walk stages as 10..15).
+// The sums live in LDS until the wave ends (WSTAMP_FLUSH): a stamp waits only
+// for LDS and scalar reads (lgkmcnt), not for the wave's outstanding global
+// loads and stores (vmcnt), so it does not add waits of its own. (Until round
+// 4 the sums were read-modify-written in global memory, and every stamp waited
+// for all the wave's stores: the stages after a store burst looked longer.)
 #define STAGES_MAX 16
 static __device__ uint64_t g_stage[1 << 16][STAGES_MAX];
-static __device__ uint64_t g_stage_last[1 << 16];
+static __shared__ uint64_t s_stage[HONU_WAVES_PER_BLOCK][STAGES_MAX + 1];  // + the last stamp
 #define STAGE_WID() ((uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + threadIdx.x / 64)
 #define WSTAMP(k)                                                          \
     do {                                                                   \
-        const uint64_t wid_ = STAGE_WID();                                 \
-        if (lane_id() == 0 && wid_ < (1 << 16)) {                          \
+        if (lane_id() == 0) {                                              \
+            uint64_t *s_ = s_stage[threadIdx.x / 64];                      \
             const uint64_t now_ = wall_clock64();                          \
-            g_stage[wid_][k] += now_ - g_stage_last[wid_];                 \
-            g_stage_last[wid_] = now_;                                     \
+            s_[k] += now_ - s_[STAGES_MAX];                                \
+            s_[STAGES_MAX] = now_;                                         \
         }                                                                  \
     } while (0)
 #define WSTAMP_START()                                                     \
     do {                                                                   \
+        if (lane_id() == 0) {                                              \
+            uint64_t *s_ = s_stage[threadIdx.x / 64];                      \
+            for (int k_ = 0; k_ < STAGES_MAX; k_++) s_[k_] = 0;            \
+            s_[STAGES_MAX] = wall_clock64();                               \
+        }                                                                  \
+    } while (0)
+#define WSTAMP_FLUSH()                                                     \
+    do {                                                                   \
         const uint64_t wid_ = STAGE_WID();                                 \
-        if (lane_id() == 0 && wid_ < (1 << 16)) g_stage_last[wid_] = wall_clock64(); \
+        if (lane_id() == 0 && wid_ < (1 << 16))                            \
+            for (int k_ = 0; k_ < STAGES_MAX; k_++)                        \
+                g_stage[wid_][k_] += s_stage[threadIdx.x / 64][k_];        \
     } while (0)
 #else
 #define WSTAMP(k) \
@@ -230,6 +245,11 @@ static __device__ uint64_t g_stage_last[1 << 16];
 #endif
 #ifndef WSTAMP_START
 #define WSTAMP_START() \
+    do {               \
+    } while (0)
+#endif
+#ifndef WSTAMP_FLUSH
+#define WSTAMP_FLUSH() \
     do {               \
     } while (0)
 #endif

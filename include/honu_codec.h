@@ -208,11 +208,19 @@ int32_t honu_ctx_reset(honu_ctx *ctx, void *stream);
  * size; 6 the single-launch decode at every size), "encode_variant" (the
  * header/tail encoder of honu_encode_records: 0 one record per lane + the ACL
  * lists by 16-lane groups, the default; 1 one record per 16-lane group laid
- * out by a prefix sum over the grammar's slots, same bytes). Also
+ * out by a prefix sum over the grammar's slots, same bytes), "speculate" (1
+ * default, 0 off: the single-launch decode's speculation, see
+ * honu_decode_records). Also
  * settable at context creation through the environment (HONU_COPY_BLOCKS,
  * HONU_RECORD_BLOCKS, HONU_LANE_BLOCKS, HONU_COPY_VARIANT, HONU_RECORD_VARIANT,
  * HONU_ENCODE_VARIANT). */
 int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value);
+
+/* The current value of a parameter of honu_ctx_set_param, and
+ * "speculate_backoff": how many of the context's next decode calls run
+ * without speculation (16 once a recovery launch has run, see
+ * honu_decode_records; the count drops by one per call). */
+int32_t honu_ctx_get_param(const honu_ctx *ctx, const char *name, int64_t *value);
 
 /* ABI self-description, used by bindings to check struct layouts. */
 uint32_t honu_abi_version(void);
@@ -330,7 +338,10 @@ int32_t honu_decode_payloads(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n,
  * were published, or a nil ACL entry, is decoded a second time without
  * speculation inside the same call, so such a batch costs about twice a
  * clean one (malformed input and nil entries only; results are exact either
- * way). */
+ * way). A recovery that ran sets a pinned word of the context, and the
+ * context's next 16 calls after the host sees it do not speculate (no
+ * recovery launch: about 1.1x a speculative clean call), so a stream of such
+ * batches does not pay twice per batch. */
 int32_t honu_decode_records(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
                             uint64_t n, honu_meta *d_meta, honu_record_info *d_info,
                             honu_acl *d_acl, uint64_t acl_cap, uint32_t *d_regions,

@@ -237,6 +237,58 @@ def test_speculative_acl_flags_recover(oracle_lib, n, k):
         c.close()
 
 
+def test_speculation_backs_off_after_a_recovery(oracle_lib):
+    """A recovery launch that ran sets the context's pinned word; the context's
+    next 16 decode calls then run without speculation (honu_decode_records),
+    and speculation resumes after them. Every call in the sequence, and a call
+    with speculation switched off by honu_ctx_set_param("speculate", 0) over a
+    batch that would misspeculate, is bit-exact with the oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ctypes as C
+    n = 140000
+    rec, off, _ = oracle_lib.marshal_batch(gen_host_batch(45, "small", 0, n))
+    bad = {9, 64 * 900 + 1}
+    pieces, noff = [], [0]
+    for i in range(n):
+        r = rec[int(off[i]):int(off[i + 1])]
+        pieces.append(r[:-3] if i in bad else r)
+        noff.append(noff[-1] + len(pieces[-1]))
+    brec, boff = np.concatenate(pieces), np.array(noff, np.uint64)
+    c = hobj.Codec(0, n)
+
+    def get(name):
+        v = C.c_int64(-1)
+        hobj._lib.check(c.lib.honu_ctx_get_param(c.ctx, name, C.byref(v)), "get_param")
+        return v.value
+    try:
+        hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
+        d, good = _Dec(c, brec, boff), _Dec(c, rec, off)
+        assert get(b"speculate") == 1 and get(b"speculate_backoff") == 0
+        assert good() == 0
+        good.check(oracle_lib, rec, off)
+        assert get(b"speculate_backoff") == 0  # a clean speculative call: no recovery
+        assert d() == 0
+        d.check(oracle_lib, brec, boff)  # synchronizes: the recovery has run
+        assert get(b"speculate_backoff") == 16
+        for k in range(16):
+            assert (good if k % 2 else d)() == 0
+            assert get(b"speculate_backoff") == 15 - k
+            if k in (0, 15):
+                (good if k % 2 else d).check(oracle_lib, *((rec, off) if k % 2 else (brec, boff)))
+        # the back-off is over: the next misspeculating call recovers again
+        assert d() == 0
+        d.check(oracle_lib, brec, boff)
+        assert get(b"speculate_backoff") == 16
+        hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"speculate", 0), "param")
+        for _ in range(17):  # run the back-off out, then no speculation at all
+            assert d() == 0
+        d.check(oracle_lib, brec, boff)
+        assert get(b"speculate") == 0 and get(b"speculate_backoff") == 0
+    finally:
+        c.close()
+
+
 def test_concurrent_ticket_and_static_launches_on_two_streams(oracle_lib):
     """Two contexts decoding at once on their own streams: ticket-mode launches
     (2188 tiles: a workgroup takes its waves' first tiles with one atomic,

@@ -3,7 +3,10 @@
 full load: the timing build (make -C honu_amd timing, -DHONU_STAGE_TIMING)
 has lane 0 of every wave add the time since its previous stamp to a stage
 counter at fixed points of every tile it takes (win.h WSTAMP 0..9 inside the
-walk, fused.hip 10..13 after it). Sum over waves / tiles = mean stage time per
+walk, fused.hip 10..15 after it; the ACL fill is 13 + 14 + 15: its rounds'
+waits (the staging DMA and every store issued before it), its passes, the
+rest). The sums are kept in LDS until the wave ends, so stamps add no waits
+for outstanding stores (win.h). Sum over waves / tiles = mean stage time per
 tile in microseconds (s_memrealtime, 100 MHz); the stages add up to the
 launch's waves x their lifetime.
 
@@ -27,7 +30,8 @@ from honu_amd.workload import gen_meta  # noqa: E402
 
 STAGES = ["ticket", "rec_off", "header", "window1", "to_acl_count", "acl_flags",
           "window_after_acl", "regions_to_sig", "window_after_sig", "tail_end",
-          "publish_rows_out", "lookback_wait", "info_regions", "acl_fill"]
+          "publish_rows_out", "lookback_wait", "info_regions", "acl_fill_rest",
+          "acl_fill_wait", "acl_fill_passes"]
 P = lambda t: t.data_ptr()  # noqa: E731
 
 
