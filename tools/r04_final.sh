@@ -8,6 +8,9 @@
 #           one TA / TD / TCP pass of it (the copy kernels' L1 path)
 #   part 2: FETCH_SIZE / WRITE_SIZE of the configs[2] zero-copy decode leg, and
 #           one bench line per README shape
+#   part 3 (after the line-drain tail encoder): the Small line's kernel-trace
+#           stats and timed steps, FETCH_SIZE / WRITE_SIZE / TA / TD of the
+#           tail encoder launched alone on 1M Small (tools/enc_timing.py)
 set -u
 out=$1; part=$2
 mkdir -p $out
@@ -42,5 +45,19 @@ if [ "$part" = 2 ]; then
   timeout -k 10 400 python bench.py --mode decode --decode-leg zero_copy --no-cpu-baseline --no-host-path \
     > $out/bench_zero_copy.json 2> $out/bench_zero_copy.err || exit 2
   tools/shape_sweep.sh $out/shapes || exit 3
+fi
+if [ "$part" = 3 ]; then
+  timeout -k 10 300 python bench.py --shape small > $out/bench_small.json 2> $out/bench_small.err || exit 1
+  timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $out/prof_small -o run --output-format csv \
+    -- python3 bench.py --shape small --no-cpu-baseline --no-host-path --no-decode-legs \
+    > $out/bench_prof_small.json 2> $out/prof_small.log || exit 2
+  tr=$(find $out/prof_small -name '*kernel_trace.csv' | head -n 1)
+  st=$(find $out/prof_small -name '*kernel_stats.csv' | head -n 1)
+  cp "$st" $out/kernel_stats_small.csv
+  python3 tools/timed_stats.py "$tr" $out/bench_prof_small.json $out/timed_kernel_stats_small.csv \
+    > $out/timed_small.txt || exit 3
+  gzip -f "$tr"
+  tools/pmc_passes.sh $out/pmc_encoder "FETCH_SIZE" "WRITE_SIZE" "TA_TA_BUSY_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE" \
+    -- python3 tools/enc_timing.py --shape small --records 1048576 --no-stamps > $out/pmc_encoder.log 2>&1 || exit 4
 fi
 exit 0
