@@ -23,6 +23,7 @@ Prints ONE JSON line on rank 0 (see DESIGN.md for every field).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import gc
 import json
 import os
@@ -366,6 +367,18 @@ class Bench:
     # chunks (box-dependent, -2 % to +4 % for the single launch) and keep the
     # encode copy faster (5.84 vs 5.63-5.67 TB/s, profiles/r02/crossover_static_tiles.txt)
     FUSED_DECODE_MIN = 128 << 10
+
+    def recoveries_seen(self):
+        """Output slots whose single-launch decode ran a recovery launch since
+        the last call (honu_ctx_get_param "speculate_backoff"; malformed input
+        only, so 0 on the bench's records); clears the back-off."""
+        seen = 0
+        for sl in self.slots:
+            v = ctypes.c_int64(0)
+            _lib.check(self.lib.honu_ctx_get_param(sl.codec.ctx, b"speculate_backoff", ctypes.byref(v)), "param")
+            _lib.check(self.lib.honu_ctx_set_param(sl.codec.ctx, b"speculate_backoff", 0), "param")
+            seen += v.value > 0
+        return seen
 
     def fused_decode(self, n):
         # beside the decode copy the persistent single-launch grid costs the copy more
@@ -1237,6 +1250,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
     for _ in range(args.warmup):
         bench.step()
     torch.cuda.synchronize()
+    bench.recoveries_seen()  # count the timed steps' only
     bench.events = []
     barrier()
     torch.cuda.synchronize()
@@ -1246,6 +1260,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    recoveries = bench.recoveries_seen()  # before anything else decodes on the slots
     # whole-job totals: every rank encodes/decodes its own records
     per_rank_s = [elapsed]
     tot = [bench.total_rec_bytes, bench.N]
@@ -1330,6 +1345,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
             "metadata_beside": bench.meta_beside,
             "metadata_streams": len(bench.sms),
             "metadata_decode": "fused" if bench.fused_decode(bench.C) else "split",
+            "decode_recoveries_in_timed_steps": recoveries,
         },
         "records_per_s": total_records / step_s,
         "ranks": ranks,

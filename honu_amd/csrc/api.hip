@@ -240,6 +240,10 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
     else if (!strcmp(name, "record_blocks") && value > 0) ctx->geom.per_record_blocks = (int)value;
     else if (!strcmp(name, "lane_blocks") && value >= 0) ctx->geom.lane_blocks = (int)value;
     else if (!strcmp(name, "speculate") && (value == 0 || value == 1)) ctx->spec_allowed = value != 0;
+    else if (!strcmp(name, "speculate_backoff") && value >= 0 && value <= (int64_t)SPEC_BACKOFF_CALLS) {
+        __atomic_store_n(ctx->spec_seen, 0u, __ATOMIC_RELAXED);
+        ctx->spec_off = (uint32_t)value;
+    }
     else if (!strcmp(name, "copy_variant") && value >= 0 && (value == 0 || HONU_AB_BUILD))
         ctx->geom.copy_variant = (int)value;
     else if (!strcmp(name, "encode_variant") && (value == 0 || value == 1))

@@ -347,7 +347,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
             // (their list offsets are patched in below)
             lb_publish<3>(lb_status, t, ep, agg);
         }
-        rows_out(ws, R, i0, lim, O.meta);
+        rows_out<true>(ws, R, i0, lim, O.meta);
         // the ACL lists with every entry present go to the table from LDS: the
         // first round of their blocks is staged now, before the wait, as it
         // needs no offsets

@@ -22,7 +22,10 @@ namespace honu {
 // Small 0.298 -> 0.265 ms; 64 K Small 0.074 -> 0.078 ms and a 62 K Large chunk
 // 0.082 -> 0.086 ms (latency-bound: fewer records in flight per SIMD and
 // lines held back lengthen a tile), hence the switch.
-constexpr uint64_t ENC_LINE_MIN_TILES = 2 * 4 * 256;  // the line form's resident waves (2 workgroups x 4 waves x 256 CUs)
+#ifndef ENC_LINE_MIN_TILES_N  // (A/B builds only)
+#define ENC_LINE_MIN_TILES_N (2 * 4 * 256)  // the line form's resident waves (2 workgroups x 4 waves x 256 CUs)
+#endif
+constexpr uint64_t ENC_LINE_MIN_TILES = ENC_LINE_MIN_TILES_N;
 template <int RING> constexpr uint32_t enc_wave_bytes() { return (RING > 0 ? RING : 1) * HONU_WAVE * 16; }
 
 template <bool SKIP_ACL, int RING>

@@ -607,7 +607,14 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
 }
 
 // The wave's 64 rows out through its LDS windows (free after the walk): 32
-// rows per pass, written as contiguous 16-byte stores.
+// rows per pass, written as contiguous 16-byte stores. NT: non-temporal
+// stores (the single-launch decode, whose rows nothing in the launch reads
+// again: 1M Small zero copy 0.704-0.711 -> 0.691-0.694 ms, 62 K Large 0.080-0.084
+// -> 0.079-0.080 ms, profiles/r04/ab/dec_nt_stores_ab.jsonl; the split parse's
+// rows are read back by its table kernel, so it keeps plain stores). (The ACL
+// table as non-temporal stores too: 1M Small equal to rows alone, 62 K Large
+// 0.085 ms, slower.)
+template <bool NT = false>
 HONU_DEV void rows_out(uint8_t *wave_smem, const Row &R, uint64_t i0, uint64_t n,
                        honu_meta *__restrict__ meta) {
     const uint32_t lane = lane_id();
@@ -624,7 +631,10 @@ HONU_DEV void rows_out(uint8_t *wave_smem, const Row &R, uint64_t i0, uint64_t n
         const uint64_t rows = r0 >= n ? 0 : (n - r0 < 32 ? n - r0 : 32);
         const u32x4 *src = reinterpret_cast<const u32x4 *>(wave_smem);
         u32x4 *out = reinterpret_cast<u32x4 *>(meta + r0);
-        for (uint32_t s = lane; s < rows * 22; s += HONU_WAVE) out[s] = src[s];
+        for (uint32_t s = lane; s < rows * 22; s += HONU_WAVE) {
+            if constexpr (NT) __builtin_nontemporal_store(src[s], out + s);
+            else out[s] = src[s];
+        }
     }
     wave_sync();
 }

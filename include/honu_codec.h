@@ -210,7 +210,9 @@ int32_t honu_ctx_reset(honu_ctx *ctx, void *stream);
  * lists by 16-lane groups, the default; 1 one record per 16-lane group laid
  * out by a prefix sum over the grammar's slots, same bytes), "speculate" (1
  * default, 0 off: the single-launch decode's speculation, see
- * honu_decode_records). Also
+ * honu_decode_records), "speculate_backoff" (0..16: the calls left without
+ * speculation after a recovery; setting it also forgets a recovery the host
+ * has not seen yet). Also
  * settable at context creation through the environment (HONU_COPY_BLOCKS,
  * HONU_RECORD_BLOCKS, HONU_LANE_BLOCKS, HONU_COPY_VARIANT, HONU_RECORD_VARIANT,
  * HONU_ENCODE_VARIANT). */
