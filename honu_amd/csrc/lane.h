@@ -221,7 +221,8 @@ HONU_DEV uint32_t uvarint_bytes(uint64_t x, uint64_t &lo, uint64_t &hi) {
 // the line is complete or the record ends, so L2 gets every interior line of
 // a tail whole, at once, instead of in pieces ~10 us apart (1M Small: HBM
 // writes 1.05 -> 0.66 GB and reads 1.28 -> 0.93 GB per launch, 1.09 -> 0.99
-// ms; DESIGN §3 "Round 4").
+// ms; DESIGN §3 "Round 4"). (The whole lines as non-temporal stores: 1M Small
+// 0.99 -> 1.37 ms, profiles/r04/ab/enc_line_nt_ab.jsonl.)
 template <int R>
 struct LaneWriterT {
     uint8_t *out;
