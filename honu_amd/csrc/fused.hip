@@ -50,7 +50,13 @@ struct DecodeOut {
 // ACL entries read as two 16-byte LDS reads and a select chain (FILL_DW 0,
 // slower); the measurement knobs that skip the fill, the look-back wait or
 // the tickets (HONU_FUSED_DBG). DESIGN §3 has the numbers.
-constexpr uint64_t FUSED_SPEC_MIN_TILES = 768;
+// (Round 4, with the grouped prefixes: 768 still right, no speculation below
+// 2049 tiles is 5-7 % slower on 62 K Large / 64 K Small, from 512 equal;
+// profiles/r04/ab/dec_spec_min_ab.jsonl.)
+#ifndef FUSED_SPEC_MIN_TILES_N  // (A/B builds only)
+#define FUSED_SPEC_MIN_TILES_N 768
+#endif
+constexpr uint64_t FUSED_SPEC_MIN_TILES = FUSED_SPEC_MIN_TILES_N;
 #ifndef FUSED_GROUP_LB
 #define FUSED_GROUP_LB 1
 #endif
