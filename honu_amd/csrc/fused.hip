@@ -77,7 +77,11 @@ static_assert(STAGE_SLOTS % HONU_WAVE == 0, "whole instructions");
 // one workgroup per CU, with twice the staging area so a tile's lists stage in
 // one round issued before the look-back wait, measured equal: 62 K Large
 // 0.081-0.085 vs 0.082-0.084 ms, 64 K XLarge 0.0735 vs 0.0732 ms,
-// profiles/r04/ab/wide_static_ab.jsonl.)
+// profiles/r04/ab/wide_static_ab.jsonl. So was a pair form for launches of at
+// most 1,024 tiles, two waves per tile, the second staging and filling every
+// second ACL round in its own LDS from a plan and offsets handed over in LDS:
+// parity green, 62 K Large 0.076-0.080 vs 0.077-0.080 ms, 64 K / 40 K / 16 K
+// Small equal, profiles/r04/ab/dec_pair_fill_ab.jsonl.)
 enum { FORM_TICKET = 0, FORM_STATIC = 1 };
 template <int FORM> constexpr uint32_t form_slots() { return STAGE_SLOTS; }
 // a wave's LDS: its windows during the walk, the staging after it
