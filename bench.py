@@ -80,6 +80,9 @@ def parse_args(argv=None):
                    help="metadata streams: 2 = one per output slot, so consecutive chunks' metadata "
                         "kernels (each slot has its own context) may run at once (round 4: Mixed "
                         "66.4 -> 58.3 ms/step, Small/Medium/Large unchanged within 0.5%%)")
+    p.add_argument("--copy-streams", type=int, default=1, choices=[1, 2],
+                   help="2: decode copies on a stream of their own, so a chunk's encode copy need "
+                        "not wait behind the previous chunk's decode copy")
     p.add_argument("--copy-prio", type=int, default=1,
                    help="1: the copy stream gets high priority; 0: neither; -1: the metadata stream does")
     p.add_argument("--meta-beside", choices=["auto", "encode", "decode"], default="auto",
@@ -241,6 +244,10 @@ class Bench:
         self.sms = [self.sm]
         if getattr(args, "meta_streams", 1) == 2 and nslots == 2 and not args.meta_cu_stride:
             self.sms.append(torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio < 0 else 0))
+        # --copy-streams 2: decode copies on their own stream
+        self.sd = self.sc
+        if getattr(args, "copy_streams", 1) == 2 and nslots == 2 and not args.meta_cu_stride:
+            self.sd = torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio > 0 else 0)
         self.sv = torch.cuda.Stream(self.dev)  # verification of drained chunks
         self.events = None
         self.last = None
@@ -283,6 +290,7 @@ class Bench:
         if pending is not None:
             ok &= self._check(check, pending)
         torch.cuda.current_stream(self.dev).wait_stream(self.sc)
+        torch.cuda.current_stream(self.dev).wait_stream(self.sd)
         for sm in self.sms:
             torch.cuda.current_stream(self.dev).wait_stream(sm)
         return ok
@@ -347,18 +355,21 @@ class Bench:
             e1.record(sc)
         self.enc_done = torch.cuda.Event()
         self.enc_done.record(sc)
-        sc.wait_event(ev_fill)
+        sd = self.sd  # the decode copy: after this chunk's encode copy and its table fill
+        if sd is not sc:
+            sd.wait_event(self.enc_done)
+        sd.wait_event(ev_fill)
         e2 = torch.cuda.Event(enable_timing=True) if timed else None
         e3 = torch.cuda.Event(enable_timing=True) if timed else None
         if timed:
-            e2.record(sc)
+            e2.record(sd)
         _lib.check(L.honu_decode_payloads(c, P(sl.out), n, P(sl.dinfo), P(sl.data),
-                                          P(sl.totals), cs), "decode_payloads")
+                                          P(sl.totals), sd.cuda_stream), "decode_payloads")
         if timed:
-            e3.record(sc)
+            e3.record(sd)
             self.events.append((a, b, e0, e1, e2, e3))
         sl.free = torch.cuda.Event()
-        sl.free.record(sc)
+        sl.free.record(sd)
         self.last = (a, b, sl)
         return sl
 
@@ -1344,6 +1355,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
             "meta_cu_stride": args.meta_cu_stride or None,
             "metadata_beside": bench.meta_beside,
             "metadata_streams": len(bench.sms),
+            "copy_streams": 1 if bench.sd is bench.sc else 2,
             "metadata_decode": "fused" if bench.fused_decode(bench.C) else "split",
             "decode_recoveries_in_timed_steps": recoveries,
         },

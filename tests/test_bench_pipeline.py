@@ -36,16 +36,20 @@ def _gpu():
 
 
 @pytest.mark.parametrize("decode", ["fused", "split"])
-@pytest.mark.parametrize("after,beside,ms", [("scan", "encode", 1), ("meta", "encode", 1), ("scan", "decode", 1),
-                                             ("scan", "encode", 2)])
+@pytest.mark.parametrize("after,beside,ms,cs", [("scan", "encode", 1, 1), ("meta", "encode", 1, 1),
+                                                ("scan", "decode", 1, 1), ("scan", "encode", 2, 1),
+                                                ("scan", "decode", 2, 1), ("scan", "encode", 2, 2),
+                                                ("scan", "decode", 2, 2)])
 @pytest.mark.parametrize("shape,n", [("small", 4000), ("mixed", 1200), ("large", 160)])
-def test_bench_pipeline_bit_exact(oracle_lib, shape, n, after, decode, beside, ms):
+def test_bench_pipeline_bit_exact(oracle_lib, shape, n, after, decode, beside, ms, cs):
     seed = 7
     args = bench.parse_args(["--records", str(n), "--shape", shape, "--min-chunks", "5",
                              "--encode-copy-after", after, "--seed", str(seed),
-                             "--decode", decode, "--meta-beside", beside, "--meta-streams", str(ms)])
+                             "--decode", decode, "--meta-beside", beside, "--meta-streams", str(ms),
+                             "--copy-streams", str(cs)])
     b = bench.Bench(args, 0, 0)
     assert len(b.chunks) >= 5 and len(b.slots) == 2 and len(b.sms) == ms
+    assert (b.sd is b.sc) == (cs == 1)
     hb = gen_host_batch(seed, shape, 0, n)  # the same records the device generator made
     seen = []
 
