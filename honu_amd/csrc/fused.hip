@@ -57,9 +57,6 @@ struct DecodeOut {
 #define FUSED_SPEC_MIN_TILES_N 768
 #endif
 constexpr uint64_t FUSED_SPEC_MIN_TILES = FUSED_SPEC_MIN_TILES_N;
-#ifndef FUSED_GROUP_LB
-#define FUSED_GROUP_LB 1
-#endif
 
 // The ACL lists (every entry present) of a tile staged into the wave's LDS
 // (its windows, free after the walk) for the table fill: round after round,
@@ -368,10 +365,9 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         WSTAMP(10);  // publish + rows out + first staging round issued
         if constexpr (STAT)  // every tile runs at once: grouped prefixes (lookback.h)
             lb_resolve_grouped<3>(lb_status, lb_gstatus, t, ntiles, ep, agg, excl);
-        else if constexpr (FUSED_GROUP_LB)  // tickets: a look-back over the group totals
+        else  // tickets: a decoupled look-back over the group totals (the plain
+              // one over tile words, lb_resolve, measured 3 % slower on 1M Small)
             lb_resolve_grouped_lb<3>(lb_status, lb_gstatus, t, ntiles, ep, agg, excl);
-        else
-            lb_resolve<3>(lb_status, t, ep, agg, excl);
         WSTAMP(11);  // look-back wait
         if (t == ntiles - 1 && lane < 3)
             O.totals[lane] = lane == 0 ? excl[0] + agg[0] : (lane == 1 ? excl[1] + agg[1] : excl[2] + agg[2]);
