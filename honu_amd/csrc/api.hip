@@ -38,6 +38,12 @@ struct honu_ctx {
     uint32_t *spec_seen;
     uint32_t spec_off;       // calls left without speculation
     bool spec_allowed;       // honu_ctx_set_param("speculate", 0) turns it off
+    // honu_encode_records: the ACL lists' kernel on a stream of the context's
+    // own, beside the header/tail encoder (forked from and joined back into
+    // the caller's stream by events)
+    hipStream_t aux;
+    hipEvent_t ev_fork, ev_join;
+    int enc_fork;            // honu_ctx_set_param("encode_fork", 0 off / 1 on / 2 auto: when lane_blocks caps the grid)
 };
 static constexpr uint32_t SPEC_BACKOFF_CALLS = 16;
 
@@ -178,6 +184,18 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     }
     *c->spec_seen = 0;
     c->spec_allowed = true;
+    c->enc_fork = env_int("HONU_ENCODE_FORK", 2);
+    if (c->enc_fork < 0 || c->enc_fork > 2) c->enc_fork = 2;
+    if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+        snprintf(g_last_error, sizeof g_last_error, "stream/event creation failed");
+        (void)hipFree(c->ws);
+        (void)hipHostFree(c->spec_seen);
+        free(c);
+        *err = HONU_E_HIP;
+        return nullptr;
+    }
     uint64_t *w = (uint64_t *)c->ws;
     c->counts = w;
     w += 3 * n;
@@ -227,6 +245,10 @@ int32_t honu_ctx_reset(honu_ctx *ctx, void *stream) {
 void honu_ctx_destroy(honu_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->aux);
+    (void)hipEventDestroy(ctx->ev_fork);
+    (void)hipEventDestroy(ctx->ev_join);
+    (void)hipStreamDestroy(ctx->aux);
     (void)hipFree(ctx->ws);
     (void)hipHostFree(ctx->spec_seen);
     free(ctx);
@@ -240,6 +262,7 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
     else if (!strcmp(name, "record_blocks") && value > 0) ctx->geom.per_record_blocks = (int)value;
     else if (!strcmp(name, "lane_blocks") && value >= 0) ctx->geom.lane_blocks = (int)value;
     else if (!strcmp(name, "speculate") && (value == 0 || value == 1)) ctx->spec_allowed = value != 0;
+    else if (!strcmp(name, "encode_fork") && value >= 0 && value <= 2) ctx->enc_fork = (int)value;
     else if (!strcmp(name, "speculate_backoff") && value >= 0 && value <= (int64_t)SPEC_BACKOFF_CALLS) {
         __atomic_store_n(ctx->spec_seen, 0u, __ATOMIC_RELAXED);
         ctx->spec_off = (uint32_t)value;
@@ -261,6 +284,7 @@ int32_t honu_ctx_get_param(const honu_ctx *ctx, const char *name, int64_t *value
     else if (!strcmp(name, "record_blocks")) *value = ctx->geom.per_record_blocks;
     else if (!strcmp(name, "lane_blocks")) *value = ctx->geom.lane_blocks;
     else if (!strcmp(name, "speculate")) *value = ctx->spec_allowed ? 1 : 0;
+    else if (!strcmp(name, "encode_fork")) *value = ctx->enc_fork;
     else if (!strcmp(name, "speculate_backoff"))  // calls the next call starts without speculation
         *value = __atomic_load_n(ctx->spec_seen, __ATOMIC_RELAXED) ? SPEC_BACKOFF_CALLS : ctx->spec_off;
     else if (!strcmp(name, "copy_variant")) *value = ctx->geom.copy_variant;
@@ -316,11 +340,28 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
     // encode_variant 0 (default, measured faster: DESIGN §3): header + tail
     // with the ACL lists' partial end chunks (one record per lane), then the
     // lists' whole chunks (16 lanes per record)
+    hipStream_t s = (hipStream_t)stream;
+    const bool fork = ctx->enc_fork == 1 || (ctx->enc_fork == 2 && ctx->geom.lane_blocks > 0);
+    if (fork && n) {
+        // the lists' whole chunks on the context's own stream, beside the
+        // header/tail encoder (disjoint bytes: the lane encoder writes the
+        // lists' partial end chunks, or skips a list with nil entries whole)
+        HIPCHK(hipEventRecord(ctx->ev_fork, s));
+        HIPCHK(hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
+        HIPCHK(launch_encode_acl_grp_self(d_meta, d_acl, d_payload_off, n, d_out, out_cap, d_out_off, d_status,
+                                          ctx->geom.lane_blocks, ctx->aux));
+        HIPCHK(hipEventRecord(ctx->ev_join, ctx->aux));
+        HIPCHK(launch_encode_meta_lane(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
+                                       out_cap, d_out_off, d_status, ctx->enc_acl,
+                                       ctx->geom.lane_blocks, s));
+        HIPCHK(hipStreamWaitEvent(s, ctx->ev_join, 0));
+        return HONU_OK;
+    }
     HIPCHK(launch_encode_meta_lane(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
                                    out_cap, d_out_off, d_status, ctx->enc_acl,
-                                   ctx->geom.lane_blocks, (hipStream_t)stream));
+                                   ctx->geom.lane_blocks, s));
     HIPCHK(launch_encode_acl_grp(d_meta, d_acl, n, d_out, d_status, ctx->enc_acl,
-                                 ctx->geom.lane_blocks, (hipStream_t)stream));
+                                 ctx->geom.lane_blocks, s));
     return HONU_OK;
 }
 

@@ -223,15 +223,44 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_grp(
 // loads, one aligned store per chunk, byte stores only at the list's ends.
 // A list with nil entries is written serially by the group's lead lane.
 // ------------------------------------------------------------------------
-template <int G>
+// SELF: the kernel places the list itself (no acl_pos from the lane
+// encoder), so it can run beside the lane encoder: the list starts after the
+// header, the payload and the tail fields up to the ACL count (the size
+// pass's prefix, k_encode_sizes_grp_one), and is written whole-chunk when
+// every entry is present (the lane encoder's own test, lane.h).
+template <int G, bool SELF>
 HONU_DEV void k_encode_acl_grp_one(uint64_t i, const honu_meta *__restrict__ meta, const honu_acl *__restrict__ acl, uint64_t n,
     uint8_t *__restrict__ out, const int32_t *__restrict__ status,
-    const uint64_t *__restrict__ acl_pos) {
+    const uint64_t *__restrict__ acl_pos, const uint64_t *__restrict__ payload_off,
+    const uint64_t *__restrict__ out_off, uint64_t out_cap) {
     const uint32_t r = threadIdx.x & (G - 1);
     // independent loads first: one round trip before the entries
     const int32_t sti = status[i];
-    const uint64_t na = meta[i].acl_count, ao = meta[i].acl_off, pos = acl_pos[i];
-    if (sti != HONU_OK || !na) return;
+    const honu_meta &m = meta[i];
+    const uint64_t na = m.acl_count, ao = m.acl_off;
+    uint64_t pos;
+    if constexpr (SELF) {
+        const uint64_t beg = out_off[i], end = out_off[i + 1];
+        if (sti != HONU_OK || !na || end > out_cap) return;  // (the lane encoder flags the capacity)
+        const uint32_t pr = m.present;
+        uint64_t t = 1 + 32 + 1;  // meta flag, ObjectID, CollectionID, Version flag
+        if (pr & HONU_HAS_VERSION)
+            t += uvarint_len(m.pid) + uvarint_len(m.vid) + uvarint_len(m.region) + 1 +
+                 ((pr & HONU_HAS_PARENT) ? uvarint_len(m.parent_pid) + uvarint_len(m.parent_vid) : 0) + 1 +
+                 uvarint_len(zigzag(m.version_created));
+        t += 1;  // Schema flag
+        if (pr & HONU_HAS_SCHEMA)
+            t += gframe_len(m.schema_name.len) + uvarint_len(m.schema_major) + uvarint_len(m.schema_minor) +
+                 uvarint_len(m.schema_patch);
+        t += gframe_len(m.mime.len) + 33 + uvarint_len(na);  // MIME, Owner, Group, Permissions, count
+        const uint64_t dlen = payload_off[i + 1] - payload_off[i];
+        uint64_t miss = 0;  // nil entries
+        for (uint64_t k = r; k < na; k += G) miss += acl[ao + k].present ? 0 : 1;
+        pos = (beg + 1 + uvarint_len(dlen) + dlen + t) | (grp_sum64<G>(miss) == 0 ? ACL_ALL_PRESENT : 0);
+    } else {
+        pos = acl_pos[i];
+        if (sti != HONU_OK || !na) return;
+    }
     const honu_acl *A = acl + ao;
     const uint64_t P = pos & ~ACL_ALL_PRESENT;
     if (pos & ACL_ALL_PRESENT) {  // whole chunks [ceil16(P), floor16(E))
@@ -269,14 +298,15 @@ HONU_DEV void k_encode_acl_grp_one(uint64_t i, const honu_meta *__restrict__ met
     }
 }
 
-template <int G>
+template <int G, bool SELF>
 __global__ __launch_bounds__(HONU_BLOCK) void k_encode_acl_grp(
     const honu_meta *__restrict__ meta, const honu_acl *__restrict__ acl, uint64_t n,
     uint8_t *__restrict__ out, const int32_t *__restrict__ status,
-    const uint64_t *__restrict__ acl_pos) {
+    const uint64_t *__restrict__ acl_pos, const uint64_t *__restrict__ payload_off,
+    const uint64_t *__restrict__ out_off, uint64_t out_cap) {
     for (uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G; i < n;
          i += (uint64_t)gridDim.x * (HONU_BLOCK / G))
-        k_encode_acl_grp_one<G>(i, meta, acl, n, out, status, acl_pos);
+        k_encode_acl_grp_one<G, SELF>(i, meta, acl, n, out, status, acl_pos, payload_off, out_off, out_cap);
 }
 
 #undef OFF
@@ -295,8 +325,17 @@ hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uin
                                  uint8_t *out, const int32_t *status, const uint64_t *acl_pos,
                                  int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_encode_acl_grp<GRP>, grp_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta, acl, n,
-                       out, status, acl_pos);
+    hipLaunchKernelGGL((k_encode_acl_grp<GRP, false>), grp_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta, acl,
+                       n, out, status, acl_pos, nullptr, nullptr, 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_encode_acl_grp_self(const honu_meta *meta, const honu_acl *acl, const uint64_t *payload_off,
+                                      uint64_t n, uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
+                                      const int32_t *status, int max_blocks, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL((k_encode_acl_grp<GRP, true>), grp_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta, acl,
+                       n, out, status, nullptr, payload_off, out_off, out_cap);
     return hipGetLastError();
 }
 

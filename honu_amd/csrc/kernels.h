@@ -118,6 +118,11 @@ hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, co
 hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uint64_t n,
                                  uint8_t *out, const int32_t *status, const uint64_t *acl_pos,
                                  int max_blocks, hipStream_t s);
+// the same with the lists placed by the kernel itself (no acl_pos), so that it
+// can run beside launch_encode_meta_lane
+hipError_t launch_encode_acl_grp_self(const honu_meta *meta, const honu_acl *acl, const uint64_t *payload_off,
+                                      uint64_t n, uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
+                                      const int32_t *status, int max_blocks, hipStream_t s);
 // header + Metadata tail, ACL entries included, one record per 16-lane group
 // (enc.hip; encode_variant 1)
 hipError_t launch_encode_tail_grp(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,

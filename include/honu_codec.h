@@ -212,7 +212,11 @@ int32_t honu_ctx_reset(honu_ctx *ctx, void *stream);
  * default, 0 off: the single-launch decode's speculation, see
  * honu_decode_records), "speculate_backoff" (0..16: the calls left without
  * speculation after a recovery; setting it also forgets a recovery the host
- * has not seen yet). Also
+ * has not seen yet), "encode_fork" (honu_encode_records: 1 runs the ACL lists'
+ * kernel, which then places the lists itself, on a stream of the context's own
+ * beside the header/tail encoder, forked from and joined back into the
+ * caller's stream by events; 0 after it; 2, the default, forks when
+ * "lane_blocks" caps the encoder's grid). Also
  * settable at context creation through the environment (HONU_COPY_BLOCKS,
  * HONU_RECORD_BLOCKS, HONU_LANE_BLOCKS, HONU_COPY_VARIANT, HONU_RECORD_VARIANT,
  * HONU_ENCODE_VARIANT). */

@@ -21,20 +21,24 @@ from honu_amd.metadata import META_DTYPE, normalize, pack_batch, unpack_row  # n
 from honu_amd.workload import gen_host_batch, gen_meta  # noqa: E402
 
 
-@pytest.fixture(scope="module", params=[(6, 0), (5, 1)], ids=["fused", "split"])
+@pytest.fixture(scope="module", params=[(6, 0, 2), (5, 1, 2), (6, 0, 1)], ids=["fused", "split", "fork"])
 def codec(request):
     """Both metadata decodes and both header/tail encoders of the product
     library: the single-launch decode (fused.hip) at every batch size with the
     default lane encoder + group ACL lists (lane.hip, grp.hip), and the split
     decode kernels (windowed lane parse, group fill) with the group-layout
     encoder (enc.hip, encode_variant 1). The default picks the decode by batch
-    size; the bench pipeline and large-batch tests run it."""
+    size; the bench pipeline and large-batch tests run it. "fork": the ACL
+    lists' kernel placing the lists itself on the context's own stream, beside
+    the lane encoder (encode_fork 1; the default 2 forks only when lane_blocks
+    caps the encoder's grid, as the bench does for large records)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     c = hobj.Codec(0, 1 << 18)
-    rv, ev = request.param
+    rv, ev, fork = request.param
     hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", rv), "param")
     hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"encode_variant", ev), "param")
+    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"encode_fork", fork), "param")
     yield c
     c.close()
 
