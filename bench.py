@@ -102,10 +102,20 @@ def parse_args(argv=None):
                         "tables (split), or by chunk size as honu_decode_batch (auto)")
     p.add_argument("--copy-blocks", type=int, default=0,
                    help="workgroups per CU of the payload copy engine (0 = library default)")
-    p.add_argument("--mode", choices=["encdec", "decode"], default="encdec",
+    p.add_argument("--mode", choices=["encdec", "decode", "encode"], default="encdec",
                    help="encdec: the encode + materialising decode step (the metric); decode: "
                         "configs[2] only, Metadata()+Data() of the whole batch from one resident "
-                        "records arena (zero copy in one call + materialising in chunks)")
+                        "records arena (zero copy in one call + materialising in chunks); encode: "
+                        "configs[3]'s step, object.Marshal of every record (size pass, the "
+                        "per-record output-offset prefix scan, headers + tails, payload copy)")
+    p.add_argument("--legs", default="auto",
+                   help="encdec mode, comma list of extra legs after the main one: small (1M Small "
+                        "encode + decode, configs[1]), mixed_encode (1M Mixed encode, configs[3]); "
+                        "auto: both for the default Large line, none otherwise; none: no legs")
+    p.add_argument("--decode-chain", type=int, default=1, choices=[0, 1],
+                   help="with two metadata streams, a chunk's single-launch decode waits for the "
+                        "previous chunk's (and its guarded launch): the guard never queues for "
+                        "LDS behind the other slot's persistent decode")
     p.add_argument("--decode-leg", choices=["both", "zero_copy", "materialising"], default="both",
                    help="decode mode: run one leg only (PMC passes attribute a kernel's traffic "
                         "to one leg)")
@@ -138,10 +148,12 @@ class Slot:
 
 
 class Bench:
-    def __init__(self, args, rank, device, pipeline=True):
+    def __init__(self, args, rank, device, pipeline=True, encode_only=False):
         """pipeline=False: inputs, chunks and sizes only (no payload arena, no
-        output slots) for DecodeBench."""
+        output slots) for DecodeBench. encode_only: the step is object.Marshal
+        of every record (configs[3]); the decode runs only in the check."""
         self.args = args
+        self.encode_only = encode_only
         self.dev = torch.device("cuda", device)
         N = args.records
         self.N = N
@@ -204,8 +216,8 @@ class Bench:
         if not pipeline:
             return
         nslots = 1 if args.serial else 2
-        self.slots = [Slot(self.dev, C, self.out_cap, self.acl_cap, self.reg_cap, self.data_cap)
-                      for _ in range(nslots)]
+        self.slots = [Slot(self.dev, C, self.out_cap, self.acl_cap, self.reg_cap,
+                           16 if encode_only else self.data_cap) for _ in range(nslots)]
         ncu = torch.cuda.get_device_properties(self.dev).multi_processor_count
         lane_blocks = args.lane_blocks
         if lane_blocks < 0:  # measured: tools/overlap_sweep.sh, tools/ab_env.sh, tools/args_ab.sh
@@ -253,6 +265,7 @@ class Bench:
         self.last = None
         self.nchunk = 0  # chunks issued so far, across steps: slots alternate globally
         self.enc_done = None  # the last issued chunk's encode copy (--meta-beside decode)
+        self.dec_done = None  # the last issued chunk's single-launch decode (--decode-chain)
         torch.cuda.synchronize()
 
     def _sizes(self, codec, a, b, out_off, status, s):
@@ -318,9 +331,14 @@ class Bench:
         if self.meta_beside == "decode" and self.enc_done is not None:
             sm.wait_event(self.enc_done)
         ms = sm.cuda_stream
+        if timed and self.encode_only:
+            o0, o1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            o0.record(sm)
         self._sizes(sl.codec, a, b, sl.out_off, sl.status, ms)
         ev_off = torch.cuda.Event()
         ev_off.record(sm)
+        if timed and self.encode_only:
+            o1.record(sm)
         _lib.check(L.honu_encode_records(c, P(self.meta) + 352 * a, P(self.var), P(self.acl),
                                          P(self.reg), P(self.off) + 8 * a, n, P(sl.out),
                                          self.out_cap, P(sl.out_off), P(sl.status), ms),
@@ -328,11 +346,23 @@ class Bench:
         if self.args.encode_copy_after == "meta":
             ev_off = torch.cuda.Event()
             ev_off.record(sm)
+        if self.encode_only:
+            return self._issue_encode_copy(a, b, sl, sm, timed, ev_off, (o0, o1) if timed else None)
         if self.fused_decode(n):  # parse + look-back + tables in one launch (fused.hip)
+            # with two metadata streams the previous chunk's decode (and its
+            # guarded launch) finishes first: a guard that is a no-op would
+            # otherwise wait up to ~1 ms for LDS this decode's persistent grid
+            # holds, and hold up its stream meanwhile
+            chain = self.args.decode_chain and len(self.sms) > 1
+            if chain and self.dec_done is not None:
+                sm.wait_event(self.dec_done)
             _lib.check(L.honu_decode_records(c, P(sl.out), P(sl.out_off), n, P(sl.dmeta),
                                              P(sl.dinfo), P(sl.dacl), self.acl_cap, P(sl.dreg),
                                              self.reg_cap, 1, self.data_cap, P(sl.totals), ms),
                        "decode_records")
+            if chain:
+                self.dec_done = torch.cuda.Event()
+                self.dec_done.record(sm)
         else:
             _lib.check(L.honu_decode_parse(c, P(sl.out), P(sl.out_off), n, P(sl.dmeta),
                                            P(sl.dinfo), ms), "decode_parse")
@@ -373,23 +403,48 @@ class Bench:
         self.last = (a, b, sl)
         return sl
 
+    def _issue_encode_copy(self, a, b, sl, sm, timed, ev_off, off_events):
+        """encode_only: the payload copy of chunk [a, b) after its offsets; the
+        slot frees when it is done."""
+        L, n = self.lib, b - a
+        sc = self.sc
+        sc.wait_event(ev_off)
+        e0 = torch.cuda.Event(enable_timing=True) if timed else None
+        e1 = torch.cuda.Event(enable_timing=True) if timed else None
+        if timed:
+            e0.record(sc)
+        _lib.check(L.honu_encode_payloads(sl.codec.ctx, P(self.payload), P(self.off) + 8 * a, n,
+                                          P(sl.out), self.out_cap, P(sl.out_off), P(sl.status),
+                                          sc.cuda_stream), "encode_payloads")
+        if timed:
+            e1.record(sc)
+            self.events.append((a, b, e0, e1) + tuple(off_events))
+        ev = torch.cuda.Event()  # the slot frees once its header/tail encoder is done too
+        ev.record(sm)
+        sc.wait_event(ev)
+        sl.free = torch.cuda.Event()
+        sl.free.record(sc)
+        self.last = (a, b, sl)
+        return sl
+
     # The pipeline's own crossover, above honu_decode_batch's 48 K: beside the
     # other chunk's copies the split kernels are as fast on 62 K-record Large
     # chunks (box-dependent, -2 % to +4 % for the single launch) and keep the
     # encode copy faster (5.84 vs 5.63-5.67 TB/s, profiles/r02/crossover_static_tiles.txt)
     FUSED_DECODE_MIN = 128 << 10
 
-    def recoveries_seen(self):
-        """Output slots whose single-launch decode ran a recovery launch since
-        the last call (honu_ctx_get_param "speculate_backoff"; malformed input
-        only, so 0 on the bench's records); clears the back-off."""
-        seen = 0
+    def recoveries(self):
+        """Recovery launches the output slots' single-launch decodes have run
+        so far (honu_ctx_get_param "recoveries": a count the guarded launch
+        increments when it runs; malformed input or nil ACL entries only, so
+        it stays put on the bench's records). The timed steps report the
+        difference across them."""
+        total = 0
         for sl in self.slots:
             v = ctypes.c_int64(0)
-            _lib.check(self.lib.honu_ctx_get_param(sl.codec.ctx, b"speculate_backoff", ctypes.byref(v)), "param")
-            _lib.check(self.lib.honu_ctx_set_param(sl.codec.ctx, b"speculate_backoff", 0), "param")
-            seen += v.value > 0
-        return seen
+            _lib.check(self.lib.honu_ctx_get_param(sl.codec.ctx, b"recoveries", ctypes.byref(v)), "param")
+            total += v.value
+        return total
 
     def fused_decode(self, n):
         # beside the decode copy the persistent single-launch grid costs the copy more
@@ -416,10 +471,15 @@ class Bench:
         (verification) stream: encode statuses OK; honu_verify_decoded of every
         decoded row, span, ACL entry and region against the source row it was
         encoded from; every materialised payload's digest equal to its
-        source's."""
+        source's. encode_only: the chunk's records are decoded here (zero
+        copy, untimed) and every Data() subslice's digest is compared."""
         L, c = self.lib, sl.codec.ctx
         n = b - a
         s = torch.cuda.current_stream(self.dev).cuda_stream
+        if self.encode_only:
+            _lib.check(L.honu_decode_batch(c, P(sl.out), P(sl.out_off), n, P(sl.dmeta), P(sl.dinfo),
+                                           P(sl.dacl), self.acl_cap, P(sl.dreg), self.reg_cap, 0, 0,
+                                           P(sl.totals), s), "decode_batch")
         st = sl.status[: 4 * n].view(torch.int32)
         info = sl.dinfo[: 32 * n].view(torch.int64).view(n, 4)
         mism = torch.empty(4 * n, dtype=torch.uint8, device=self.dev)
@@ -432,7 +492,8 @@ class Bench:
         _lib.check(L.honu_digest_records(c, P(self.payload), P(self.off) + 8 * a, 0, n, P(dsrc), s),
                    "digest")
         doff, dlen = info[:, 0].contiguous(), info[:, 1].contiguous()
-        _lib.check(L.honu_digest_records(c, P(sl.data), P(doff), P(dlen), n, P(ddst), s), "digest")
+        _lib.check(L.honu_digest_records(c, P(sl.out if self.encode_only else sl.data), P(doff), P(dlen),
+                                         n, P(ddst), s), "digest")
         ok = bool((st == 0).all()) and int(torch.count_nonzero(mism.view(torch.int32))) == 0
         ok &= torch.equal(dsrc, ddst)
         torch.cuda.current_stream(self.dev).synchronize()
@@ -585,14 +646,19 @@ class DecodeBench:
         hm = b.host_meta
         self.nacl = int(hm["acl_count"].astype(np.int64).sum())
         self.nreg = int(hm["regions_count"].astype(np.int64).sum())
-        self.meta_bytes = (8 * N + self.hdr_bytes + self.tail_bytes + 352 * N + 32 * N +
-                           20 * self.nacl + 4 * self.nreg)
         self.payload_bytes = int(plen.sum())
         # whole-batch outputs
         self.dmeta, self.dinfo = E(352 * N), E(32 * N)
         self.acl_cap, self.reg_cap = self.nacl + 1, self.nreg + 1
         self.dacl, self.dreg = E(20 * self.acl_cap), E(4 * self.reg_cap)
         self.totals = E(32)
+        # ACL table entries the default (in-place) form writes: the lists with
+        # a nil entry only (none in the generator's records), from one
+        # untimed decode
+        self._zero_copy_once(s)
+        st.synchronize()
+        self.acl_table_entries = int(self.totals[:8].view(torch.int64).item())
+        self.meta_bytes = self.meta_bytes_for(self.acl_table_entries)
         # materialising leg: two data slots of one chunk each
         self.slots = []
         for _ in range(2):
@@ -607,6 +673,16 @@ class DecodeBench:
         self.sv = torch.cuda.Stream(dev)
         torch.cuda.synchronize()
 
+    def meta_bytes_for(self, acl_table_entries):
+        """Algorithmic bytes of one Metadata() + zero-copy Data() pass (SURVEY
+        §8d): per record the offsets pair, the header and the Metadata tail
+        read; the row, the record info, 4 per region and 20 per ACL TABLE
+        entry written (a list returned in place writes nothing: its entries
+        are read as part of the tail)."""
+        N = self.b.N
+        return (8 * N + self.hdr_bytes + self.tail_bytes + 352 * N + 32 * N +
+                20 * acl_table_entries + 4 * self.nreg)
+
     # -- zero copy, whole batch ------------------------------------------------
     def _zero_copy_once(self, s):
         b, L = self.b, self.lib
@@ -615,7 +691,7 @@ class DecodeBench:
                                        P(self.dreg), self.reg_cap, 0, 0, P(self.totals), s),
                    "decode_batch")
 
-    def zero_copy(self, reps):
+    def _zero_copy_reps(self, reps):
         st = torch.cuda.current_stream(self.dev)
         self._zero_copy_once(st.cuda_stream)
         ev = []
@@ -626,16 +702,37 @@ class DecodeBench:
             e1.record(st)
             ev.append((e0, e1))
         torch.cuda.synchronize()
-        ms = [x.elapsed_time(y) for x, y in ev]
+        return [x.elapsed_time(y) for x, y in ev]
+
+    def zero_copy(self, reps):
+        """The default decode (ACL lists returned in place, HONU_ACL_INPLACE),
+        then the same call with every list copied into the ACL table (context
+        param acl_inplace 0, the form of rounds 1-4) for comparison."""
+        c = self.codec.ctx
+        _lib.check(self.lib.honu_ctx_set_param(c, b"acl_inplace", 0), "param")
+        ms_tab = self._zero_copy_reps(reps)
+        tab_entries = int(self.totals[:8].view(torch.int64).item())
+        _lib.check(self.lib.honu_ctx_set_param(c, b"acl_inplace", 1), "param")
+        ms = self._zero_copy_reps(reps)
         t = sum(ms) / len(ms) / 1e3
+        t_tab = sum(ms_tab) / len(ms_tab) / 1e3
         N = self.b.N
         gbs = self.meta_bytes / t / 1e9
+        tab_bytes = self.meta_bytes_for(tab_entries)
         return {
             "records": N,
             "reps": reps,
             "ms": t * 1e3,
             "ms_min": min(ms),
             "records_per_s": N / t,
+            "acl_form": (f"in place (HONU_ACL_INPLACE): lists with every entry present stay in the "
+                         f"records arena; {self.acl_table_entries} ACL table entries written"),
+            "acl_table_form": {"ms": t_tab * 1e3, "ms_min": min(ms_tab), "records_per_s": N / t_tab,
+                               "acl_table_entries": tab_entries,
+                               "algorithmic_bytes_per_launch": tab_bytes,
+                               "frac_of_spec": tab_bytes / t_tab / 1e9 / HBM_PEAK_GBS,
+                               "how": "the same call with acl_inplace 0: every list copied into "
+                                      "the 20-byte ACL table (rounds 1-4)"},
             "calls": "honu_decode_batch(data arena NULL) over all records, one call",
             "roofline": {
                 "bound": "hbm",
@@ -649,7 +746,8 @@ class DecodeBench:
                 "avg_launch_ms": t * 1e3,
                 "algorithmic_bytes_per_launch": self.meta_bytes,
                 "algorithmic_bytes": "8 (offsets) + header + Metadata tail read; 352 row + 32 info "
-                                     "+ 20 per ACL entry + 4 per region written, per record",
+                                     "+ 4 per region + 20 per ACL TABLE entry written, per record "
+                                     "(in-place lists: none)",
             },
         }
 
@@ -1072,6 +1170,8 @@ def main(argv=None):
 
     if args.mode == "decode":
         result = decode_mode(args, rank, local, world, dist, barrier, gather_max, all_ok)
+    elif args.mode == "encode":
+        result = encode_mode(args, rank, local, world, dist, barrier, gather_max, all_ok)
     else:
         result = encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok)
     if result is not None and rank == 0:
@@ -1235,6 +1335,160 @@ def decode_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
     }
 
 
+LEG_SHAPES = {"small": ("small", False), "mixed_encode": ("mixed", True)}
+
+
+def legs_of(args):
+    """The extra legs of an encdec line (--legs): configs[1] (1M Small encode
+    + decode) and configs[3] (1M Mixed encode) ride along with the default
+    1M Large line, so that the driver's own run measures them too."""
+    if args.legs == "none":
+        return []
+    if args.legs == "auto":
+        default = args.shape == "large" and args.records == 1 << 20 and args.mode == "encdec"
+        return list(LEG_SHAPES) if default else []
+    legs = [x.strip() for x in args.legs.split(",") if x.strip()]
+    for x in legs:
+        if x not in LEG_SHAPES:
+            raise SystemExit(f"bench.py: unknown leg {x!r} (known: {', '.join(LEG_SHAPES)})")
+    return legs
+
+
+def pipeline_leg(args, shape, encode_only, rank, local, world, dist, barrier, gather_max, all_ok):
+    """One timed pipelined configuration of this rank's --records records of
+    `shape` (a Bench of its own, released at the end): warmup, barrier, the
+    timed steps, barrier; max over ranks. encode_only: object.Marshal only
+    (configs[3]: size pass, output-offset prefix scan, headers + tails,
+    payload copy), else encode + materialising decode (configs[1]). Returns
+    the leg's dict (value in GiB/s of records over all ranks, the dominant
+    copy kernel's roofline, the whole step's algorithmic HBM fraction)."""
+    la = argparse.Namespace(**vars(args))
+    la.shape = shape
+    bench = Bench(la, rank, local, encode_only=encode_only)
+    for _ in range(la.warmup):
+        bench.step()
+    torch.cuda.synchronize()
+    rec0 = bench.recoveries()
+    bench.events = []
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(la.steps):
+        bench.step(timed=True)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    recoveries = bench.recoveries() - rec0
+    elapsed, per_rank = gather_max(elapsed)
+    tot = [bench.total_rec_bytes, bench.N, bench.payload_bytes]
+    if dist is not None:
+        tt = torch.tensor(tot, dtype=torch.int64, device=bench.dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        tot = [int(x) for x in tt.tolist()]
+    step_s = elapsed / la.steps
+    pay = [2 * bench.chunk_payload[bench.chunks.index((a, b))] for (a, b, *_) in bench.events]
+    enc_ms = [x[2].elapsed_time(x[3]) for x in bench.events]
+    other_ms = [x[4].elapsed_time(x[5]) for x in bench.events]  # decode copy / offsets
+    enc_gbs = sum(pay) / (sum(enc_ms) / 1e3) / 1e9
+    verified = None if la.no_verify else bench.verify()
+    bench.release()
+    verified = all_ok(verified)
+    what = "encode (object.Marshal)" if encode_only else \
+        "encode (object.Marshal) + materialising decode (Object.Metadata + Object.Data)"
+    workload = f"{bench.N} {shape} records per GPU: {what}"
+    kern, kms, kgbs = "k_copy_segments<honu::EncodeSegments>", enc_ms, enc_gbs
+    if not encode_only and sum(other_ms) > sum(enc_ms):
+        kern, kms = "k_copy_segments<honu::DecodeSegments>", other_ms
+        kgbs = sum(pay) / (sum(other_ms) / 1e3) / 1e9
+    # the step's algorithmic HBM bytes: encode reads rows + inputs and writes
+    # the records (~2 x record bytes), the decode reads them and writes rows +
+    # payloads (~2 x record bytes again)
+    step_bytes = (2 if encode_only else 4) * bench.total_rec_bytes
+    out = {
+        "workload": workload,
+        "records_per_gpu": bench.N,
+        "shape": shape,
+        "chunks": len(bench.chunks),
+        "steps": la.steps,
+        "warmup": la.warmup,
+        "ms_per_step": step_s * 1e3,
+        "per_rank_ms_per_step": [x / la.steps * 1e3 for x in per_rank],
+        "value": tot[0] / step_s / 2**30,
+        "unit": "GiB/s",
+        "records_per_s": tot[1] / step_s,
+        "encoded_bytes_per_gpu": bench.total_rec_bytes,
+        "payload_bytes_per_gpu": bench.payload_bytes,
+        "step_hbm_gbs_algorithmic": step_bytes / step_s / 1e9,
+        "step_frac_of_spec": step_bytes / step_s / 1e9 / HBM_PEAK_GBS,
+        "step_bytes": f"{'2' if encode_only else '4'} x encoded record bytes per GPU",
+        "roofline": {
+            "bound": "hbm",
+            "kernel": kern,
+            "achieved": kgbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": kgbs / HBM_PEAK_GBS,
+            "traffic": pmc_traffic(workload, kern.split(">")[0]),
+            "launches": len(kms),
+            "avg_launch_ms": sum(kms) / max(1, len(kms)),
+            "algorithmic_bytes_per_launch": sum(pay) / max(1, len(pay)),
+        },
+        "encode_copy_gbs": enc_gbs,
+        "metadata_decode": None if encode_only else ("fused" if bench.fused_decode(bench.C) else "split"),
+        "decode_recoveries_in_timed_steps": None if encode_only else recoveries,
+        "verified": verified,
+        "verified_scope": None if verified is None else Bench.VERIFIED_SCOPE + (
+            " (the records decoded untimed, zero copy, for the check)" if encode_only else ""),
+    }
+    if encode_only:  # configs[3] names the per-record output-offset prefix scan
+        out["offsets_ms_per_step"] = sum(other_ms) / la.steps
+        out["offsets"] = ("size pass (k_encode_sizes_grp) + exclusive scan (k_scan_lb) of every "
+                          "chunk, on the metadata stream, events around both")
+    else:
+        out["decode_copy_gbs"] = sum(pay) / (sum(other_ms) / 1e3) / 1e9
+    return out
+
+
+def run_legs(args, rank, local, world, dist, barrier, gather_max, all_ok):
+    legs = {}
+    for name in legs_of(args):
+        shape, enc = LEG_SHAPES[name]
+        gc.collect()
+        torch.cuda.empty_cache()
+        legs[name] = pipeline_leg(args, shape, enc, rank, local, world, dist, barrier, gather_max,
+                                  all_ok)
+    return legs or None
+
+
+def encode_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
+    """configs[3] alone: object.Marshal of this rank's records per step."""
+    leg = pipeline_leg(args, args.shape, True, rank, local, world, dist, barrier, gather_max, all_ok)
+    if rank != 0:
+        return None
+    return {
+        "metric": METRIC,
+        "value": leg["value"],
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": leg["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: seeded generator mirroring object_test.go:195-386, payload bytes "
+                "generated on device",
+        "config": {"workload": leg["workload"], "records_per_gpu": leg["records_per_gpu"],
+                   "shape": args.shape, "chunks": leg["chunks"],
+                   "parallelism": f"dp{world} (records sharded, no data-path collective)"},
+        "records_per_s": leg["records_per_s"],
+        "roofline": leg["roofline"],
+        "encode": leg,
+        "verified": leg["verified"],
+    }
+
+
 class _Estimate:
     """N, first and an estimate of the encoded bytes of this rank's records
     (payload of a 4 K-record sample + ~1.1 KB of header and Metadata each),
@@ -1261,7 +1515,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
     for _ in range(args.warmup):
         bench.step()
     torch.cuda.synchronize()
-    bench.recoveries_seen()  # count the timed steps' only
+    rec0 = bench.recoveries()  # count the timed steps' only
     bench.events = []
     barrier()
     torch.cuda.synchronize()
@@ -1271,7 +1525,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
-    recoveries = bench.recoveries_seen()  # before anything else decodes on the slots
+    recoveries = bench.recoveries() - rec0  # before anything else decodes on the slots
     # whole-job totals: every rank encodes/decodes its own records
     per_rank_s = [elapsed]
     tot = [bench.total_rec_bytes, bench.N]
@@ -1309,6 +1563,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
     bench.release()
     decode = None if args.no_decode_legs else decode_legs(bench, args, world, barrier, gather_max,
                                                           all_ok)
+    legs = run_legs(args, rank, local, world, dist, barrier, gather_max, all_ok)
     if rank != 0:
         return None
     if decode is not None and decode.get("materialising") is not None:  # the copy's achievable rate too
@@ -1396,6 +1651,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
         "verified": ok_all,
         "verified_scope": None if ok_all is None else Bench.VERIFIED_SCOPE,
         "decode": decode,
+        "legs": legs,
         "host_path": host_path,
         "scatter": scatter,
     }

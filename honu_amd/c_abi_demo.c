@@ -14,7 +14,10 @@
  * (d_totals: the entries the batch needs), tables re-allocated to exactly
  * those and a second call -> D2H of rows/info/tables -> honu_decode_batch
  * materialising -> D2H of payloads; checks every status, the decoded rows'
- * scalar fields against the input rows and every payload's digest. With
+ * scalar fields against the input rows, every ACL list as the binding builds
+ * its []*AccessControl (acl_entry: from the records arena for a list returned
+ * in place, HONU_ACL_INPLACE, else from the ACL table) against the input
+ * entries, and every payload's digest. With
  * dump_dir, the records arena, offsets and the zero-copy outputs are written
  * there (rec.bin, off.bin, meta.bin, info.bin, acl.bin, reg.bin, tot.bin) for
  * tests/test_c_abi.py to compare with the oracle. Exit 0 and one "ok" line on
@@ -51,6 +54,25 @@ static int dump(const char *dir, const char *name, const void *p, uint64_t bytes
     if (!f) return 1;
     const int bad = bytes && fwrite(p, 1, bytes, f) != bytes;
     return fclose(f) != 0 || bad;
+}
+
+/* Entry j of a decoded row's ACL list, as the binding's Go code builds
+ * &AccessControl{ClientID, Permissions} (nil when *present == 0): in place,
+ * the 18 bytes 01 | ClientID | Permissions at acl_off + 18 j of the records
+ * arena; otherwise row j of the list in the ACL table. */
+static void acl_entry(const honu_meta *m, const uint8_t *rec, const honu_acl *table, uint64_t j,
+                      uint8_t client_id[16], uint8_t *perm, uint8_t *present) {
+    if (m->present & HONU_ACL_INPLACE) {
+        const uint8_t *e = rec + m->acl_off + 18 * j;
+        *present = e[0];
+        memcpy(client_id, e + 1, 16);
+        *perm = e[17];
+        return;
+    }
+    const honu_acl *a = table + m->acl_off + j;
+    *present = a->present;
+    memcpy(client_id, a->client_id, 16);
+    *perm = a->permissions;
 }
 
 static void *h2d(const void *h, uint64_t bytes) {
@@ -158,11 +180,12 @@ int main(int argc, char **argv) {
     CHECK(honu_memcpy_d2h(tacl, d_tacl, sizeof(honu_acl) * totals[0], NULL));
     CHECK(honu_memcpy_d2h(treg, d_treg, 4 * totals[1], NULL));
     CHECK(honu_stream_sync(NULL));
+    /* the records arena: Data(), the spans and in-place ACL lists point into it */
+    uint8_t *rec = (uint8_t *)honu_host_alloc(rec_bytes + 16);
+    NEED(rec);
+    CHECK(honu_memcpy_d2h(rec, d_out, rec_bytes, NULL));
+    CHECK(honu_stream_sync(NULL));
     if (dump_dir) {
-        uint8_t *rec = (uint8_t *)honu_host_alloc(rec_bytes + 16);
-        NEED(rec);
-        CHECK(honu_memcpy_d2h(rec, d_out, rec_bytes, NULL));
-        CHECK(honu_stream_sync(NULL));
         if (dump(dump_dir, "rec.bin", rec, rec_bytes) || dump(dump_dir, "off.bin", off, 8 * (n + 1)) ||
             dump(dump_dir, "meta.bin", meta, sizeof(honu_meta) * n) ||
             dump(dump_dir, "info.bin", info, sizeof(honu_record_info) * n) ||
@@ -171,8 +194,8 @@ int main(int argc, char **argv) {
             fprintf(stderr, "cannot write %s\n", dump_dir);
             return 1;
         }
-        honu_host_free(rec);
     }
+    uint64_t lists_inplace = 0, lists_table = 0;
     for (uint64_t i = 0; i < n; i++) {
         const honu_meta *a = rows + i, *b = meta + i;
         if (info[i].meta_status != HONU_OK || info[i].data_status != HONU_OK ||
@@ -183,6 +206,18 @@ int main(int argc, char **argv) {
                     (unsigned long long)i, info[i].meta_status, info[i].data_status);
             return 1;
         }
+        for (uint64_t j = 0; j < b->acl_count; j++) {
+            uint8_t cid[16], perm, present;
+            acl_entry(b, rec, tacl, j, cid, &perm, &present);
+            const honu_acl *src = acl + a->acl_off + j;
+            if (present != src->present || (present && (perm != src->permissions ||
+                                                        memcmp(cid, src->client_id, 16) != 0))) {
+                fprintf(stderr, "record %llu: ACL entry %llu differs\n", (unsigned long long)i,
+                        (unsigned long long)j);
+                return 1;
+            }
+        }
+        if (b->acl_count) (b->present & HONU_ACL_INPLACE) ? lists_inplace++ : lists_table++;
     }
     CHECK(honu_decode_batch(ctx, d_out, d_off, n, d_meta, d_info, d_tacl, acl_cap, d_treg,
                             reg_cap, d_data, data_cap, d_tot, NULL));
@@ -200,9 +235,11 @@ int main(int argc, char **argv) {
         }
     }
     printf("ok: %llu records, %llu encoded bytes, marshal + decode + materialise through the C ABI; "
-           "decode calls %d, table bytes %llu (ACL entries %llu, regions %llu)\n",
+           "decode calls %d, table bytes %llu (ACL entries %llu, regions %llu); ACL lists in place "
+           "%llu, in the table %llu\n",
            (unsigned long long)n, (unsigned long long)rec_bytes, calls, (unsigned long long)table_bytes,
-           (unsigned long long)totals[0], (unsigned long long)totals[1]);
+           (unsigned long long)totals[0], (unsigned long long)totals[1],
+           (unsigned long long)lists_inplace, (unsigned long long)lists_table);
     honu_ctx_destroy(ctx);
     return 0;
 }

@@ -35,7 +35,7 @@ struct honu_ctx {
     // *spec_seen (pinned host word, written by the device); the next call sees
     // it and decodes SPEC_BACKOFF_CALLS calls without speculation, so a stream
     // of batches with malformed records pays ~1.1x instead of ~2x per batch
-    uint32_t *spec_seen;
+    uint32_t *spec_seen;     // pinned: [0] the back-off flag, [1] recovery launches run (a count)
     uint32_t spec_off;       // calls left without speculation
     bool spec_allowed;       // honu_ctx_set_param("speculate", 0) turns it off
     // honu_encode_records: the ACL lists' kernel on a stream of the context's
@@ -44,6 +44,7 @@ struct honu_ctx {
     hipStream_t aux;
     hipEvent_t ev_fork, ev_join;
     int enc_fork;            // honu_ctx_set_param("encode_fork", 0 off / 1 on / 2 auto: when lane_blocks caps the grid)
+    bool acl_inplace;        // honu_ctx_set_param("acl_inplace"): decode returns all-present ACL lists in place
 };
 static constexpr uint32_t SPEC_BACKOFF_CALLS = 16;
 
@@ -144,6 +145,22 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
         return nullptr;
     }
     honu_ctx *c = (honu_ctx *)calloc(1, sizeof(honu_ctx));
+    if (!c) {
+        *err = HONU_E_HIP;
+        return nullptr;
+    }
+    // every failure below ends here: whatever was created is destroyed
+    auto fail = [&](int32_t e, const char *what) -> honu_ctx * {
+        if (what) snprintf(g_last_error, sizeof g_last_error, "%s", what);
+        if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+        if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+        if (c->aux) (void)hipStreamDestroy(c->aux);
+        if (c->spec_seen) (void)hipHostFree(c->spec_seen);
+        if (c->ws) (void)hipFree(c->ws);
+        free(c);
+        *err = e;
+        return nullptr;
+    };
     c->device = device;
     c->max_n = max_records ? max_records : 1;
     c->geom.num_cu = prop.multiProcessorCount;
@@ -152,9 +169,10 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->geom.copy_blocks = env_int("HONU_COPY_BLOCKS", prop.multiProcessorCount * 2);
     c->geom.copy_variant = HONU_AB_BUILD ? env_int("HONU_COPY_VARIANT", 0) : 0;
     c->geom.record_variant = env_int("HONU_RECORD_VARIANT", 0);
-    c->geom.encode_variant = env_int("HONU_ENCODE_VARIANT", 0) == 1 ? 1 : 0;  // 0 default
+    c->geom.encode_variant = HONU_AB_BUILD && env_int("HONU_ENCODE_VARIANT", 0) == 1 ? 1 : 0;  // 0 default
     if (c->geom.record_variant != 5 && c->geom.record_variant != 6)
         c->geom.record_variant = 0;
+    c->acl_inplace = env_int("HONU_ACL_INPLACE", 1) != 0;
     const uint64_t n = c->max_n;
     const uint64_t np = 0;
     const uint64_t map_cap = HONU_AB_BUILD ? 1ull << 22 : 0;  // tile map (A/B sweep copy)
@@ -168,33 +186,32 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     const uint64_t bytes = 8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 32 * n +
                            8 * n + 4 * map_cap + lb_bytes + 256;
     if (hipMalloc(&c->ws, bytes) != hipSuccess) {
-        snprintf(g_last_error, sizeof g_last_error, "hipMalloc(%llu) failed",
-                 (unsigned long long)bytes);
-        free(c);
-        *err = HONU_E_HIP;
-        return nullptr;
+        c->ws = nullptr;
+        char msg[96];
+        snprintf(msg, sizeof msg, "hipMalloc(%llu) failed", (unsigned long long)bytes);
+        return fail(HONU_E_HIP, msg);
     }
-    if (hipHostMalloc((void **)&c->spec_seen, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+    if (hipHostMalloc((void **)&c->spec_seen, 2 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
         hipSuccess) {
-        snprintf(g_last_error, sizeof g_last_error, "hipHostMalloc(spec_seen) failed");
-        (void)hipFree(c->ws);
-        free(c);
-        *err = HONU_E_HIP;
-        return nullptr;
+        c->spec_seen = nullptr;
+        return fail(HONU_E_HIP, "hipHostMalloc(spec_seen) failed");
     }
-    *c->spec_seen = 0;
+    c->spec_seen[0] = 0;
+    c->spec_seen[1] = 0;
     c->spec_allowed = true;
     c->enc_fork = env_int("HONU_ENCODE_FORK", 2);
     if (c->enc_fork < 0 || c->enc_fork > 2) c->enc_fork = 2;
-    if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
-        snprintf(g_last_error, sizeof g_last_error, "stream/event creation failed");
-        (void)hipFree(c->ws);
-        (void)hipHostFree(c->spec_seen);
-        free(c);
-        *err = HONU_E_HIP;
-        return nullptr;
+    if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) {
+        c->aux = nullptr;
+        return fail(HONU_E_HIP, "stream creation failed");
+    }
+    if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess) {
+        c->ev_fork = nullptr;
+        return fail(HONU_E_HIP, "event creation failed");
+    }
+    if (hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+        c->ev_join = nullptr;
+        return fail(HONU_E_HIP, "event creation failed");
     }
     uint64_t *w = (uint64_t *)c->ws;
     c->counts = w;
@@ -224,13 +241,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     ok = ok && hipMemsetAsync(c->lb_dec, 0, lb_bytes, s) == hipSuccess;
     ok = ok && hipStreamSynchronize(s) == hipSuccess;
     if (s) (void)hipStreamDestroy(s);
-    if (!ok) {
-        (void)hipFree(c->ws);
-        (void)hipHostFree(c->spec_seen);
-        free(c);
-        *err = HONU_E_HIP;
-        return nullptr;
-    }
+    if (!ok) return fail(HONU_E_HIP, "look-back state initialisation failed");
     return c;
 }
 
@@ -263,13 +274,14 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
     else if (!strcmp(name, "lane_blocks") && value >= 0) ctx->geom.lane_blocks = (int)value;
     else if (!strcmp(name, "speculate") && (value == 0 || value == 1)) ctx->spec_allowed = value != 0;
     else if (!strcmp(name, "encode_fork") && value >= 0 && value <= 2) ctx->enc_fork = (int)value;
+    else if (!strcmp(name, "acl_inplace") && (value == 0 || value == 1)) ctx->acl_inplace = value != 0;
     else if (!strcmp(name, "speculate_backoff") && value >= 0 && value <= (int64_t)SPEC_BACKOFF_CALLS) {
         __atomic_store_n(ctx->spec_seen, 0u, __ATOMIC_RELAXED);
         ctx->spec_off = (uint32_t)value;
     }
     else if (!strcmp(name, "copy_variant") && value >= 0 && (value == 0 || HONU_AB_BUILD))
         ctx->geom.copy_variant = (int)value;
-    else if (!strcmp(name, "encode_variant") && (value == 0 || value == 1))
+    else if (!strcmp(name, "encode_variant") && (value == 0 || (value == 1 && HONU_AB_BUILD)))
         ctx->geom.encode_variant = (int)value;
     else if (!strcmp(name, "record_variant") &&
              (value == 0 || value == 5 || value == 6))
@@ -285,6 +297,9 @@ int32_t honu_ctx_get_param(const honu_ctx *ctx, const char *name, int64_t *value
     else if (!strcmp(name, "lane_blocks")) *value = ctx->geom.lane_blocks;
     else if (!strcmp(name, "speculate")) *value = ctx->spec_allowed ? 1 : 0;
     else if (!strcmp(name, "encode_fork")) *value = ctx->enc_fork;
+    else if (!strcmp(name, "acl_inplace")) *value = ctx->acl_inplace ? 1 : 0;
+    else if (!strcmp(name, "recoveries"))  // recovery launches that ran, since the context was created
+        *value = __atomic_load_n(ctx->spec_seen + 1, __ATOMIC_RELAXED);
     else if (!strcmp(name, "speculate_backoff"))  // calls the next call starts without speculation
         *value = __atomic_load_n(ctx->spec_seen, __ATOMIC_RELAXED) ? SPEC_BACKOFF_CALLS : ctx->spec_off;
     else if (!strcmp(name, "copy_variant")) *value = ctx->geom.copy_variant;
@@ -331,12 +346,14 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
     if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
     HIPCHK(hipSetDevice(ctx->device));
     if (n > ctx->max_n) return HONU_E_WORKSPACE;
-    if (ctx->geom.encode_variant == 1) {  // one launch, 16 lanes per record (enc.hip)
+#ifdef HONU_AB
+    if (ctx->geom.encode_variant == 1) {  // one launch, 16 lanes per record (enc.hip, A/B build only)
         HIPCHK(launch_encode_tail_grp(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
                                       out_cap, d_out_off, d_status, ctx->geom.lane_blocks,
                                       (hipStream_t)stream));
         return HONU_OK;
     }
+#endif
     // encode_variant 0 (default, measured faster: DESIGN §3): header + tail
     // with the ACL lists' partial end chunks (one record per lane), then the
     // lists' whole chunks (16 lanes per record)
@@ -419,7 +436,7 @@ int32_t honu_decode_parse(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(launch_decode_parse_win(d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
                                    ctx->reg_inline, ctx->counts, ctx->geom.lane_blocks,
-                                   (hipStream_t)stream));
+                                   ctx->acl_inplace, (hipStream_t)stream));
     return HONU_OK;
 }
 
@@ -499,7 +516,8 @@ int32_t honu_decode_records(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t 
     HIPCHK(launch_decode_fused(d_rec, d_rec_off, n, d_meta, d_info, d_acl, acl_cap, d_regions,
                                regions_cap, materialize != 0, data_cap, ctx->scratch, ctx->offs,
                                tot, ctx->lb_dec, ctx->lb_dec_status, ctx->lb_dec_gstatus,
-                               ctx->lb_dec_words, fused_blocks(ctx->geom), ctx->spec_seen, spec, s));
+                               ctx->lb_dec_words, fused_blocks(ctx->geom), ctx->spec_seen,
+                               ctx->spec_seen + 1, spec, ctx->acl_inplace, s));
     return HONU_OK;
 }
 

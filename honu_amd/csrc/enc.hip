@@ -33,6 +33,10 @@
 // same, byte for byte (tests/test_gpu_parity.py runs both).
 #include "grp.h"
 
+// Measured slower than the default encoder (below), so it is built only into
+// the A/B library (make ab, -DHONU_AB) as encode_variant 1.
+#ifdef HONU_AB
+
 namespace honu {
 
 enum : uint8_t {
@@ -381,3 +385,4 @@ hipError_t launch_encode_tail_grp(const honu_meta *meta, const uint8_t *var, con
 #undef OFF
 
 }  // namespace honu
+#endif  // HONU_AB

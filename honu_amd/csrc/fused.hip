@@ -227,6 +227,56 @@ struct AclStage {
     }
 };
 
+// In-place ACL lists (HONU_ACL_INPLACE): the speculative walk took every list
+// that fits as all present; its flags are checked here. flag_gather fetches
+// the dwords holding flags [from, from + 64) of every lane's list (base: the
+// list's first flag, cnt: its entries, 0 for none) into the wave's LDS, 256
+// bytes per list: instruction k has lane j fetch flag j of lane k's list (a
+// few cache lines per instruction, the lines the list occupies anyway).
+HONU_DEV void flag_gather(uint8_t *ws, const uint8_t *__restrict__ rec, uint64_t base, uint64_t cnt,
+                          uint64_t from) {
+    const uint32_t lane = lane_id();
+    const uint64_t b = base + 18 * from;
+    const uint32_t m = cnt > from ? (uint32_t)(cnt - from < HONU_WAVE ? cnt - from : HONU_WAVE) : 0;
+#pragma unroll 4
+    for (uint32_t k = 0; k < HONU_WAVE; k++) {
+        const uint32_t mk = __builtin_amdgcn_readlane(m, k);
+        if (!mk) continue;  // wave-uniform
+        const uint64_t bk = readlane64(b, k);
+        if (lane < mk)
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(rec + ((bk + 18ull * lane) & ~3ull)),
+                (__attribute__((address_space(3))) void *)(ws + 256 * k), 4, 0, 0);
+    }
+}
+// After flag_gather(.., 0): true when a flag of this lane's list (chk) is not
+// 1 (a nil entry or a bad flag: the walk then read the fields after the list
+// at the wrong place). Lists of more than 64 entries take further bursts.
+// Leaves the LDS free.
+HONU_DEV bool flag_check(uint8_t *ws, const uint8_t *__restrict__ rec, bool chk, uint64_t base,
+                         uint64_t cnt) {
+    const uint32_t lane = lane_id();
+    bool bad = false;
+    for (uint64_t from = 0;; from += HONU_WAVE) {
+        __builtin_amdgcn_s_waitcnt(0);  // the burst has landed
+        wave_sync();
+        if (chk && cnt > from) {
+            const uint32_t m = (uint32_t)(cnt - from < HONU_WAVE ? cnt - from : HONU_WAVE);
+            const uint64_t b = base + 18 * from;
+            const __attribute__((address_space(3))) uint8_t *fl =
+                (const __attribute__((address_space(3))) uint8_t *)(ws + 256 * lane);
+#pragma unroll
+            for (uint32_t j = 0; j < HONU_WAVE; j++)
+                if (j < m) bad |= fl[4 * j + (uint32_t)((b + 18ull * j) & 3)] != 1;
+        }
+        if (!__ballot(chk && cnt > from + HONU_WAVE)) break;
+        wave_sync();  // every lane has read its flags before the next burst lands
+        flag_gather(ws, rec, chk ? base : 0, chk ? cnt : 0, from + HONU_WAVE);
+    }
+    wave_sync();
+    return bad;
+}
+
 // Speculative publish (the walk's early hook): a tile's counts go to the
 // look-back as soon as its regions are read, ~18 us per tile before the walk
 // ends, so successors wait less. A record failing in a later field has its
@@ -259,18 +309,21 @@ struct SpecPub {
 // tiles and grouped prefixes instead of tickets and the look-back over group
 // totals (lookback.h); each form a kernel of its own, so none pays another's
 // registers or LDS.
-template <int MODE, int FORM>
+template <int MODE, int FORM, bool INPL>
 __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
     DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t *lb_gstatus, uint64_t lb_words,
-    uint32_t *spec_seen) {
+    uint32_t *spec_seen, uint32_t *recoveries) {
     constexpr int mode = MODE;
     if (mode == 2 && __hip_atomic_load(&lb->misspec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
         return;  // every wave of the launch returns: the look-back state is untouched
     // a recovery that runs tells the host (the context's pinned word), which
     // then decodes the context's next calls without speculation (api.hip)
-    if (mode == 2 && spec_seen && blockIdx.x == 0 && threadIdx.x == 0)
+    if (mode == 2 && spec_seen && blockIdx.x == 0 && threadIdx.x == 0) {
         __hip_atomic_store(spec_seen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // (a count apart from the back-off flag, for measurements)
+        if (recoveries) __hip_atomic_fetch_add(recoveries, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     constexpr bool STAT = FORM != FORM_TICKET;
     constexpr uint32_t WAVE_BYTES = form_wave_bytes<FORM>();
     __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * WAVE_BYTES];
@@ -332,7 +385,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         early.status = lb_status;
         early.t = t;
         early.ep = ep;
-        win_walk(i0, ws, rec, lim, H, R, P, early);
+        win_walk(i0, ws, rec, lim, H, R, P, early, INPL);
 
         // counts -> offsets: wave scan + look-back across tiles
         uint64_t agg[3], excl[3], x0, x1, x2;
@@ -343,10 +396,10 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
             agg[0] = early.agg[0];
             agg[1] = early.agg[1];
             agg[2] = early.agg[2];
-            if (__ballot(P.nacl != early.c0 || P.nreg != early.c1) && lane == 0)
+            if (__ballot(P.ntab != early.c0 || P.nreg != early.c1) && lane == 0)
                 __hip_atomic_store(&lb->misspec, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            const uint64_t c0 = P.nacl, c1 = P.nreg, c2 = (P.data_len + 15) & ~15ull;
+            const uint64_t c0 = P.ntab, c1 = P.nreg, c2 = (P.data_len + 15) & ~15ull;
             x0 = wave_excl(c0, agg[0]);
             x1 = wave_excl(c1, agg[1]);
             x2 = wave_excl(c2, agg[2]);
@@ -355,13 +408,23 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
             lb_publish<3>(lb_status, t, ep, agg);
         }
         rows_out<true>(ws, R, i0, lim, O.meta);
-        // the ACL lists with every entry present go to the table from LDS: the
-        // first round of their blocks is staged now, before the wait, as it
-        // needs no offsets
-        const bool fl = valid && P.st == HONU_OK && P.nacl && (P.acl_pos & GRP_ACL_FAST);
+        // table form (acl_inplace 0): the ACL lists with every entry present
+        // go to the table from LDS; the first round of their blocks is staged
+        // now, before the wait, as it needs no offsets
+        const bool fl = !INPL && valid && P.st == HONU_OK && P.ntab && (P.acl_pos & GRP_ACL_FAST);
         AclStage<form_slots<FORM>()> S;
-        S.init(fl, P.acl_pos & GRP_POS_MASK, P.nacl);
+        S.init(fl, P.acl_pos & GRP_POS_MASK, P.ntab);
         if (S.more()) S.issue(ws, rec);
+        // in-place form: a speculated list stays where it is, but its entry
+        // flags must be 1. The first 64 flags of every such list come in ONE
+        // burst now (instruction k: lane j fetches the dword holding flag j of
+        // lane k's list into LDS), checked after the look-back wait, so the
+        // round trip hides under the wait and no table bytes are written.
+        // (The two forms never stage at once: an in-place list has ntab 0.)
+        const bool ichk = INPL && early.spec_acl && valid && P.st == HONU_OK && P.nacl &&
+                          (P.acl_pos & GRP_ACL_FAST);
+        const bool igather = INPL && early.spec_acl && __ballot(ichk);  // wave-uniform
+        if (igather) flag_gather(ws, rec, ichk ? (P.acl_pos & GRP_POS_MASK) : 0, ichk ? P.nacl : 0, 0);
         WSTAMP(10);  // publish + rows out + first staging round issued
         if constexpr (STAT)  // every tile runs at once: grouped prefixes (lookback.h)
             lb_resolve_grouped<3>(lb_status, lb_gstatus, t, ntiles, ep, agg, excl);
@@ -369,15 +432,21 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
               // one over tile words, lb_resolve, measured 3 % slower on 1M Small)
             lb_resolve_grouped_lb<3>(lb_status, lb_gstatus, t, ntiles, ep, agg, excl);
         WSTAMP(11);  // look-back wait
+        // nothing is staged in the in-place form: the next ticket is requested
+        // here, and the rest of the tile hides its round trip
+        if (!stat_idx && igather) {
+            tk = lb_ticket_issue(lb);
+            tk_pending = true;
+        }
         if (t == ntiles - 1 && lane < 3)
             O.totals[lane] = lane == 0 ? excl[0] + agg[0] : (lane == 1 ? excl[1] + agg[1] : excl[2] + agg[2]);
         const uint64_t ao = excl[0] + x0, ro = excl[1] + x1, doff = excl[2] + x2;
 
         int32_t mst = P.st;
         if (mst == HONU_OK) {  // as honu_decode_tables: offsets first, then the capacity check
-            if (P.nacl) O.meta[i].acl_off = ao;
+            if (P.ntab) O.meta[i].acl_off = ao;
             if (P.nreg) O.meta[i].regions_off = ro;
-            if (ao + P.nacl > O.acl_cap || ro + P.nreg > O.reg_cap) mst = HONU_ERR_CAPACITY;
+            if (ao + P.ntab > O.acl_cap || ro + P.nreg > O.reg_cap) mst = HONU_ERR_CAPACITY;
         }
         int32_t dst_ = P.data_status;
         uint64_t doff_out = P.data_off, dlen_out = P.data_len;
@@ -420,10 +489,10 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         // than one round): the lane walks its list from global memory
         const uint64_t apos = P.acl_pos & GRP_POS_MASK;
         bool acl_bad = false;  // spec_acl: an entry flag that is not 1
-        if (ok && P.nacl && !S.staged()) {
+        if (ok && P.ntab && !S.staged()) {
             uint64_t p = apos;
             const bool fast_list = (P.acl_pos & GRP_ACL_FAST) != 0;
-            for (uint64_t k = 0; k < P.nacl; k++) {
+            for (uint64_t k = 0; k < P.ntab; k++) {
                 uint32_t *d = reinterpret_cast<uint32_t *>(O.acl + ao + k);
                 if (early.spec_acl && fast_list && rec[p] != 1) acl_bad = true;
                 if (rec[p]) {
@@ -440,7 +509,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
                     p += 1;
                 }
             }
-        } else if (early.spec_acl && valid && P.st == HONU_OK && P.nacl && (P.acl_pos & GRP_ACL_FAST) &&
+        } else if (early.spec_acl && valid && P.st == HONU_OK && P.ntab && (P.acl_pos & GRP_ACL_FAST) &&
                    !S.staged()) {
             // the record failed the capacity check, so nothing is stored, but
             // its speculated list's flags still decide whether the walk read
@@ -453,6 +522,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
                 }
         }
         WSTAMP(12);  // info, regions, lists with nil entries
+        if (igather) acl_bad |= flag_check(ws, rec, ichk, P.acl_pos & GRP_POS_MASK, P.nacl);
         // staged lists: round by round, lane e of a pass takes entry e of the
         // round's entries (one run of the table per record), reads its 17
         // bytes from LDS and stores the 20-byte row
@@ -501,7 +571,7 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
                                uint64_t data_cap, DecodeScratch *scratch, uint64_t *offs,
                                uint64_t *totals, LbState *lb, uint64_t *lb_status,
                                uint64_t *lb_gstatus, uint64_t lb_words, int max_blocks, uint32_t *spec_seen,
-                               bool allow_spec, hipStream_t s) {
+                               uint32_t *recoveries, bool allow_spec, bool inplace, hipStream_t s) {
     if (n == 0) return hipSuccess;
     // (32-record tiles for batches whose 64-record tiles fill at most half the
     // resident waves, so that every SIMD walks records, measured slower with
@@ -518,12 +588,15 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
     // (profiles/r03/fused_spec_ab.jsonl, spec_acl_ab*.jsonl)
     const bool stat = tiles <= b * HONU_WAVES_PER_BLOCK && tiles <= (uint64_t)HONU_WAVE * LB_GROUPS;
     const dim3 grid((unsigned)b), block(HONU_BLOCK);
+#define HONU_FUSED_LAUNCH_F(M, F, I)                                                                      \
+    hipLaunchKernelGGL((k_decode_fused<M, F, I>), grid, block, 0, s, rec, rec_off, n, O, lb, lb_status,    \
+                       lb_gstatus, lb_words, spec_seen, recoveries)
 #define HONU_FUSED_LAUNCH(M)                                                                               \
     do {                                                                                                   \
-        if (stat) hipLaunchKernelGGL((k_decode_fused<M, FORM_STATIC>), grid, block, 0, s, rec, rec_off, n,  \
-                                     O, lb, lb_status, lb_gstatus, lb_words, spec_seen);                   \
-        else hipLaunchKernelGGL((k_decode_fused<M, FORM_TICKET>), grid, block, 0, s, rec, rec_off, n, O,   \
-                                lb, lb_status, lb_gstatus, lb_words, spec_seen);                           \
+        if (stat && inplace) HONU_FUSED_LAUNCH_F(M, FORM_STATIC, true);                                     \
+        else if (stat) HONU_FUSED_LAUNCH_F(M, FORM_STATIC, false);                                          \
+        else if (inplace) HONU_FUSED_LAUNCH_F(M, FORM_TICKET, true);                                        \
+        else HONU_FUSED_LAUNCH_F(M, FORM_TICKET, false);                                                    \
     } while (0)
     if (tiles < FUSED_SPEC_MIN_TILES || !allow_spec) {
         HONU_FUSED_LAUNCH(0);
@@ -533,6 +606,7 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
     // record failed after publishing its counts: malformed input only)
     HONU_FUSED_LAUNCH(1);
     HONU_FUSED_LAUNCH(2);
+#undef HONU_FUSED_LAUNCH_F
 #undef HONU_FUSED_LAUNCH
     return hipGetLastError();
 }

@@ -54,6 +54,7 @@ HONU_DEV void k_encode_sizes_grp_one(uint64_t i, uint8_t *smem, const honu_meta 
         const uint64_t ao = m.acl_off, ro = m.regions_off;
         if (na) ok = ok && ao <= acl_len && na <= acl_len - ao;
         if (nr) ok = ok && ro <= reg_len && nr <= reg_len - ro;
+        ok = ok && !(pr & HONU_ACL_INPLACE);  // a decode output row: its list is not in the table
         if (!ok) {
             stc = HONU_ERR_INPUT;
         } else {

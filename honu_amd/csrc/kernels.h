@@ -84,9 +84,8 @@ struct LaunchGeom {
                             // (0: one block per 256 lanes of work, no cap)
     int copy_blocks;        // blocks of the byte-balanced copy kernel
     int copy_variant;       // copy engine variant (copy.hip: unroll depth / cache policy)
-    int encode_variant;     // header/tail encoder: 0 lane writer + ACL group kernel, 1 group encoder
-                            // (enc.hip)
-                            // (lane.hip, grp.hip; default), 1 group layout (enc.hip)
+    int encode_variant;     // header/tail encoder: 0 lane writer + ACL group kernel (lane.hip,
+                            // grp.hip; default), 1 group layout (enc.hip, A/B build only)
     int record_variant;     // per-record kernels: 0 auto (the fastest measured form
                             // of each; honu_decode_batch single-launch from 48 K
                             // records), 5 split decode, 6 single-launch decode
@@ -124,7 +123,7 @@ hipError_t launch_encode_acl_grp_self(const honu_meta *meta, const honu_acl *acl
                                       uint64_t n, uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
                                       const int32_t *status, int max_blocks, hipStream_t s);
 // header + Metadata tail, ACL entries included, one record per 16-lane group
-// (enc.hip; encode_variant 1)
+// (enc.hip; encode_variant 1, A/B build only)
 hipError_t launch_encode_tail_grp(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
                                   const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
                                   uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
@@ -148,12 +147,13 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
                                uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap, int materialize,
                                uint64_t data_cap, DecodeScratch *scratch, uint64_t *offs,
                                uint64_t *totals, LbState *lb, uint64_t *lb_status,
-                               uint64_t *lb_gstatus, uint64_t lb_words, int max_blocks, uint32_t *spec_seen, bool allow_spec, hipStream_t s);
+                               uint64_t *lb_gstatus, uint64_t lb_words, int max_blocks, uint32_t *spec_seen,
+                               uint32_t *recoveries, bool allow_spec, bool inplace, hipStream_t s);
 
 hipError_t launch_decode_parse_win(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                    honu_meta *meta, honu_record_info *info,
                                    DecodeScratch *scratch, uint32_t *reg_inline, uint64_t *counts,
-                                   int max_blocks, hipStream_t s);
+                                   int max_blocks, bool inplace, hipStream_t s);
 
 hipError_t launch_system_sizes(const honu_collection *rows, uint64_t var_len, const honu_acl *acl,
                                uint64_t acl_len, const uint32_t *reg, uint64_t reg_len,

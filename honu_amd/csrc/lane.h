@@ -437,6 +437,7 @@ HONU_DEV int32_t encode_check(const honu_meta &m, uint64_t var_len, uint64_t acl
     const uint64_t ao = m.acl_off, ro = m.regions_off;
     if (na) ok = ok && ao <= acl_len && na <= acl_len - ao;
     if (nr) ok = ok && ro <= reg_len && nr <= reg_len - ro;
+    ok = ok && !(pr & HONU_ACL_INPLACE);  // a decode output row: its list is not in the table
     return ok ? HONU_OK : HONU_ERR_INPUT;
 }
 

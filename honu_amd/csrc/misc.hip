@@ -97,7 +97,9 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_digest(const uint8_t *__restrict
 // nil (fields of nil structs stay zero, metadata.go:202-302), REGIONS_NONNIL
 // added (region.go:160). Span offsets index different arenas and are not
 // compared; their bytes are. ACL entries and regions are compared entry by
-// entry through both rows' list offsets.
+// entry through both rows' list offsets; a list the decode returned in place
+// (HONU_ACL_INPLACE, allowed only when every source entry is present) is
+// compared with its 18-byte encodings in the records arena.
 // ------------------------------------------------------------------------
 constexpr uint32_t G_ALWAYS = 0, G_IGNORE = 0xFFFFFFFFu, G_ZERO = 0xFFFFFFFEu;
 
@@ -158,7 +160,11 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_verify_decoded(
         uint32_t bad = 0;
         if (inf.data_status != HONU_OK || inf.meta_status != HONU_OK) bad |= HONU_VERIFY_STATUS;
         if (inf.data_len != payload_off[i + 1] - payload_off[i]) bad |= HONU_VERIFY_STATUS;
-        if (D.present != pr) bad |= HONU_VERIFY_PRESENT;
+        bool any_nil = false;
+        for (uint64_t j = lane; pr && j < S.acl_count; j += HONU_WAVE) any_nil |= !src_acl[S.acl_off + j].present;
+        const bool all_present = pr && S.acl_count && !__ballot(any_nil);
+        const bool inpl = all_present && D.present == (pr | HONU_ACL_INPLACE);
+        if (D.present != pr && !inpl) bad |= HONU_VERIFY_PRESENT;
         bool row_bad = false;
         for (uint32_t b = lane; b < sizeof(honu_meta); b += HONU_WAVE) {
             const uint32_t g = row_gate(b);
@@ -177,7 +183,13 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_verify_decoded(
             }
             if (__ballot(span_bad)) bad |= HONU_VERIFY_SPANS;
             bool acl_bad = false;
-            for (uint64_t j = lane; j < S.acl_count; j += HONU_WAVE) {
+            for (uint64_t j = lane; inpl && j < S.acl_count; j += HONU_WAVE) {
+                const honu_acl &a = src_acl[S.acl_off + j];
+                const uint8_t *e = rec + D.acl_off + 18 * j;
+                acl_bad |= e[0] != 1 || e[17] != a.permissions;
+                for (int q = 0; q < 16; q++) acl_bad |= e[1 + q] != a.client_id[q];
+            }
+            for (uint64_t j = lane; !inpl && j < S.acl_count; j += HONU_WAVE) {
                 const honu_acl &a = src_acl[S.acl_off + j], &e = dec_acl[D.acl_off + j];
                 const uint32_t *ew = reinterpret_cast<const uint32_t *>(&e);
                 const uint32_t *aw = reinterpret_cast<const uint32_t *>(&a);

@@ -228,6 +228,7 @@ static int32_t put_plan(const honu_put_feed *f, const honu_meta *row, const uint
             if (sv.len && (!var || sv.off > var_len || sv.len > var_len - sv.off)) return HONU_ERR_INPUT;
             p.span_bytes += sv.len;
         }
+        if (row->present & HONU_ACL_INPLACE) return HONU_ERR_INPUT;  // a decode output row (table form only)
         p.nacl = row->acl_count;
         p.nreg = row->regions_count;
         if (p.nacl && (!acl || row->acl_off > acl_len || p.nacl > acl_len - row->acl_off))

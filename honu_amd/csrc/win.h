@@ -285,6 +285,7 @@ struct NoEarly {
 struct WinParse {
     int st;             // Metadata() status; HONU_SKIP for a lane past n
     uint64_t nacl, nreg;
+    uint64_t ntab;      // ACL table entries: nacl, or 0 for a list returned in place
     uint64_t acl_pos;   // first ACL entry flag, | GRP_ACL_FAST when every entry is present
     uint64_t reg_pos;   // first region varint, | GRP_REG_INLINE when nreg <= REG_INLINE
     uint32_t regs[REG_INLINE];
@@ -327,10 +328,15 @@ HONU_DEV void tile_head_bytes(const uint8_t *__restrict__ rec, TileHead &H) {
 // of record i0 + lane, the lani walk of metadata.go:202-302. Wave-uniform
 // call (every lane of the wave, i0 the same): the window refills need the
 // whole wave. H: the tile's bounds and header bytes (tile_head_*). The row
-// goes to R (RegRow, acl_off / regions_off not yet set).
+// goes to R (RegRow, regions_off not yet set; acl_off only for a list returned
+// in place). inplace (wave-uniform): a list whose entries are all present is
+// returned in place (HONU_ACL_INPLACE, acl_off = its absolute position, no
+// table entries); with early.spec_acl that is speculated like the rest of the
+// list's layout and the caller checks the flags.
 template <class RowT, class EarlyT>
 HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restrict__ rec,
-                       uint64_t n, const TileHead &H, RowT &R, WinParse &P, EarlyT &early) {
+                       uint64_t n, const TileHead &H, RowT &R, WinParse &P, EarlyT &early,
+                       bool inplace) {
 #define OFF(f) ((int)offsetof(honu_meta, f))
 #define STEP(x)                      \
     do {                             \
@@ -508,9 +514,15 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
             }
         }
     }
+    bool inpl = false;  // returned in place
     if (hm && st == HONU_OK && nacl > 0) {
         if (fast) {
             D.p += 18 * nacl;
+            if (inplace) {  // metadata.go:254-266 without the copy: the entries stay where they are
+                inpl = true;
+                pr |= HONU_ACL_INPLACE;
+                R.u64(OFF(acl_off), acl_pos);
+            }
             acl_pos |= GRP_ACL_FAST;  // for the fill
         } else {
             for (uint64_t k = 0; k < nacl && st == HONU_OK; k++) {
@@ -545,7 +557,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
     // both list counts are known here; a later field can still fail the
     // record (its counts then become 0): the early hook publishes them
     // tentatively (fused.hip speculative decode)
-    early.counts(hm && st == HONU_OK ? nacl : 0, hm && st == HONU_OK ? nreg : 0,
+    early.counts(hm && st == HONU_OK && !inpl ? nacl : 0, hm && st == HONU_OK ? nreg : 0,
                  (P.data_len + 15) & ~15ull);
     if (hm) {
         STEP(D.boolean(f));                                 // :271 Publisher
@@ -599,6 +611,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
     WSTAMP(9);  // walk done
     P.st = st;
     P.nacl = nacl;
+    P.ntab = inpl ? 0 : nacl;
     P.nreg = nreg;
     P.acl_pos = acl_pos;
     P.reg_pos = reg_pos;

@@ -65,6 +65,7 @@ HAS_PUBLISHER = 1 << 4
 HAS_ENCRYPTION = 1 << 5
 HAS_COMPRESSION = 1 << 6
 REGIONS_NONNIL = 1 << 7
+ACL_INPLACE = 1 << 8  # decode output: the ACL list in place in the records arena (honu_codec.h)
 
 SPAN_FIELDS = ("schema_name", "mime", "ip_address", "user_agent", "public_key_id",
                "encryption_key", "hmac_secret", "signature")
@@ -291,7 +292,9 @@ def _ulid(b) -> bytes:
 
 def unpack_row(row, arena, acl_table=None, regions_table=None) -> Metadata:
     """Rebuild a Metadata from a decoded row; spans index `arena`, lists the
-    decoded tables. Mirrors the nil/empty rules of the Go decoder
+    decoded tables, or `arena` for an ACL list returned in place
+    (ACL_INPLACE: entry j = the 18 bytes 01 | ClientID | Permissions at
+    acl_off + 18 j). Mirrors the nil/empty rules of the Go decoder
     (lani/decode.go:37-39, metadata.go:254, region.go:160)."""
     pr = int(row["present"])
     m = Metadata()
@@ -310,11 +313,25 @@ def unpack_row(row, arena, acl_table=None, regions_table=None) -> Metadata:
     m.ObjectID = bytes(row["object_id"])
     m.CollectionID = bytes(row["collection_id"])
     m.MIME = ss("mime")
-    unpack_common(row, m, sb, ss, acl_table, regions_table)
+    unpack_common(row, m, sb, ss, acl_table, regions_table, arena)
     return m
 
 
-def unpack_common(row, m, sb, ss, acl_table, regions_table):
+def acl_inplace_entries(arena, off: int, count: int) -> list:
+    """The AccessControl list of a row returned in place (ACL_INPLACE):
+    what Metadata.Decode builds from those bytes (metadata.go:254-266,
+    acls.go:41-51), each entry copied out of the records arena."""
+    arena = memoryview(arena)
+    out = []
+    for j in range(count):
+        e = bytes(arena[off + 18 * j: off + 18 * j + 18])
+        if len(e) != 18 or e[0] != 1:
+            raise ValueError("in-place ACL entry %d is not a present entry" % j)
+        out.append(AccessControl(e[1:17], e[17]))
+    return out
+
+
+def unpack_common(row, m, sb, ss, acl_table, regions_table, arena=None):
     """Inverse of pack_common on a decoded row (Go decoder nil/empty rules)."""
     pr = int(row["present"])
     if pr & HAS_VERSION:
@@ -329,7 +346,9 @@ def unpack_common(row, m, sb, ss, acl_table, regions_table):
     m.Group = bytes(row["group"])
     m.Permissions = int(row["permissions"])
     na = int(row["acl_count"])
-    if na:
+    if na and pr & ACL_INPLACE:
+        m.ACL = acl_inplace_entries(arena, int(row["acl_off"]), na)
+    elif na:
         m.ACL = []
         base = int(row["acl_off"])
         for j in range(na):

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define HONU_ABI_VERSION 3u
+#define HONU_ABI_VERSION 4u  /* 4: ACL lists returned in place (HONU_ACL_INPLACE) */
 #define HONU_STORAGE_VERSION 1u /* object.StorageVersion, object.go:14 */
 #define HONU_ULID_LEN 16
 #define HONU_KEY_LEN 29         /* keys.keySize, keys/keys.go:14 */
@@ -92,8 +92,10 @@ enum {
     HONU_HAS_PUBLISHER = 1u << 4,   /* Metadata.Publisher    metadata.go:28 */
     HONU_HAS_ENCRYPTION = 1u << 5,  /* Metadata.Encryption   metadata.go:29 */
     HONU_HAS_COMPRESSION = 1u << 6, /* Metadata.Compression  metadata.go:30 */
-    HONU_REGIONS_NONNIL = 1u << 7   /* set by decode: Regions.Decode always makes a
+    HONU_REGIONS_NONNIL = 1u << 7,  /* set by decode: Regions.Decode always makes a
                                        (possibly empty) slice, region.go:160 */
+    HONU_ACL_INPLACE = 1u << 8      /* set by decode (honu_meta only): the ACL list is
+                                       returned in place, see honu_meta.acl_off */
 };
 
 /* One metadata.Metadata (metadata.go:17-35) flattened into a fixed 352-byte
@@ -101,7 +103,22 @@ enum {
  *   encode: spans index `var_arena`, acl_off/acl_count index the ACL table,
  *           regions_off/regions_count index the region table.
  *   decode: spans are ABSOLUTE offsets into the records arena (zero copy, like
- *           lani.DecodeFixed), acl_off/regions_off index the output tables.
+ *           lani.DecodeFixed), regions_off indexes the output region table.
+ *           The ACL list comes back in one of two forms:
+ *           - in place (HONU_ACL_INPLACE set in `present`; the default, context
+ *             param "acl_inplace" 1): every entry of the list is present, and
+ *             acl_off is the ABSOLUTE offset in the records arena of the first
+ *             entry's encoding; entry j is the 18 bytes at acl_off + 18*j:
+ *             0x01 | ClientID[16] | Permissions (acls.go:26-51), so
+ *             ACL[j] = &AccessControl{rec[acl_off+18j+1 : +17], rec[acl_off+18j+17]};
+ *           - table (HONU_ACL_INPLACE clear, acl_count > 0): a list holding a
+ *             nil entry, or every list when "acl_inplace" is 0: acl_off indexes
+ *             the honu_acl output table (present == 0 is a nil entry).
+ *           Go copies every entry into a new *AccessControl either way
+ *           (metadata.go:254-266); the in-place form leaves that copy to the
+ *           binding, as Data() and the string spans already do.
+ *           Encode input rows must use the table form: a row with
+ *           HONU_ACL_INPLACE set gets HONU_ERR_INPUT from honu_encode_sizes.
  * Times are Go UnixNano with 0 <=> time.Time{}.IsZero() (lani/encode.go:201-206,
  * decode.go:224-237). Fields of absent (nil) sub-structs are zero on decode. */
 typedef struct honu_meta {
@@ -142,7 +159,8 @@ typedef struct honu_meta {
     honu_span encryption_key;    /* 272 Encryption.EncryptionKey */
     honu_span hmac_secret;       /* 288 Encryption.HMACSecret */
     honu_span signature;         /* 304 Encryption.Signature */
-    uint64_t acl_off;            /* 320 first entry in the ACL table */
+    uint64_t acl_off;            /* 320 first entry in the ACL table, or (decode,
+                                        HONU_ACL_INPLACE) in the records arena */
     uint64_t acl_count;          /* 328 len(Metadata.ACL); 0 <=> nil */
     uint64_t regions_off;        /* 336 first entry in the region table */
     uint64_t regions_count;      /* 344 len(Metadata.WriteRegions) */
@@ -219,7 +237,10 @@ int32_t honu_ctx_reset(honu_ctx *ctx, void *stream);
  * "lane_blocks" caps the encoder's grid). Also
  * settable at context creation through the environment (HONU_COPY_BLOCKS,
  * HONU_RECORD_BLOCKS, HONU_LANE_BLOCKS, HONU_COPY_VARIANT, HONU_RECORD_VARIANT,
- * HONU_ENCODE_VARIANT). */
+ * HONU_ENCODE_VARIANT). "acl_inplace" (1 default, 0 off): the decode calls
+ * (honu_decode_parse/fill/tables/records/batch) return an ACL list whose
+ * entries are all present in place (HONU_ACL_INPLACE, see honu_meta) instead
+ * of copying it into the ACL table; 0 returns every list in the table. */
 int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value);
 
 /* The current value of a parameter of honu_ctx_set_param, and
@@ -312,8 +333,9 @@ int32_t honu_decode_parse(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
  * the ACL and region tables, and when d_data != NULL assign every payload a
  * 16-byte aligned offset in d_data (d_info[i].data_off is then relative to
  * d_data) and copy the payloads there (honu_decode_payloads). d_totals
- * (device, 3 x u64) receives the totals the batch needs: ACL entries, region
- * entries, data-arena bytes (the latter also in zero-copy mode). Records whose
+ * (device, 3 x u64) receives the totals the batch needs: ACL table entries
+ * (lists returned in place take none), region entries, data-arena bytes (the
+ * latter also in zero-copy mode). Records whose
  * outputs do not fit get HONU_ERR_CAPACITY in meta_status / data_status. */
 int32_t honu_decode_fill(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
                          uint64_t n, honu_meta *d_meta, honu_record_info *d_info,

@@ -178,6 +178,7 @@ static int encode_meta(owriter *w, const honu_meta *m, const uint8_t *var, uint6
     if (m->regions_count &&
         (m->regions_off > regions_len || m->regions_count > regions_len - m->regions_off))
         bad = 1;
+    if (m->present & HONU_ACL_INPLACE) bad = 1; /* a decode output row: encode takes the table form */
     if (bad) return HONU_ERR_INPUT;
 
     w_bool(w, 1);                         /* EncodeStruct(meta) flag, encode.go:210-216 */
@@ -379,8 +380,10 @@ typedef struct {
 
 #define TRY(x) do { int st_ = (x); if (st_) return st_; } while (0)
 
-/* Metadata.Decode (metadata.go:202-302) after its nil flag. */
-static int decode_meta_body(oreader *r, uint64_t base, honu_meta *m, olists *L) {
+/* Metadata.Decode (metadata.go:202-302) after its nil flag. acl_inplace: a
+ * list whose entries are all present is returned in place (HONU_ACL_INPLACE,
+ * acl_off = absolute offset of its first entry) instead of in the table. */
+static int decode_meta_body(oreader *r, uint64_t base, honu_meta *m, olists *L, int acl_inplace) {
     int b;
     TRY(r_ulid(r, m->object_id));                    /* :210 */
     TRY(r_ulid(r, m->collection_id));                /* :214 */
@@ -417,18 +420,30 @@ static int decode_meta_body(oreader *r, uint64_t base, honu_meta *m, olists *L) 
     if (nacl > 0) {                                  /* :254-265 */
         /* make([]*AccessControl, nACLs): 8-byte elements > maxAlloc panics */
         if (nacl > GO_MAX_ALLOC / 8) return HONU_ERR_PANIC;
-        m->acl_off = L->acl_n;
-        for (uint64_t i = 0; i < nacl; i++) {
-            honu_acl a;
-            memset(&a, 0, sizeof a);
-            TRY(r_bool(r, &b));                      /* DecodeStruct(o.ACL[i]) */
-            if (b) {
-                a.present = 1;
-                TRY(r_ulid(r, a.client_id));         /* acls.go:41-51 */
-                TRY(r_byte(r, &a.permissions));
+        /* Every entry present (flag 1, then 16 + 1 bytes) with the list inside
+         * the record: exactly the lists Go decodes without a nil entry and
+         * without an error, 18 bytes per entry. */
+        int all = acl_inplace && nacl <= (r->len - r->i) / 18;
+        for (uint64_t i = 0; all && i < nacl; i++)
+            if (r->buf[r->i + 18 * i] != 1) all = 0;
+        if (all) {
+            m->present |= HONU_ACL_INPLACE;
+            m->acl_off = base + r->i;
+            r->i += 18 * nacl;
+        } else {
+            m->acl_off = L->acl_n;
+            for (uint64_t i = 0; i < nacl; i++) {
+                honu_acl a;
+                memset(&a, 0, sizeof a);
+                TRY(r_bool(r, &b));                  /* DecodeStruct(o.ACL[i]) */
+                if (b) {
+                    a.present = 1;
+                    TRY(r_ulid(r, a.client_id));     /* acls.go:41-51 */
+                    TRY(r_byte(r, &a.permissions));
+                }
+                if (L->acl_n < L->acl_cap) L->acl_out[L->acl_n] = a;
+                L->acl_n++;
             }
-            if (L->acl_n < L->acl_cap) L->acl_out[L->acl_n] = a;
-            L->acl_n++;
         }
         m->acl_count = nacl;
     }
@@ -495,7 +510,7 @@ static void data_length(const uint8_t *o, uint64_t len, int64_t *d, int64_t *b) 
 void oracle_decode(const uint8_t *o, uint64_t len, uint64_t base, honu_meta *m,
                    honu_record_info *info, honu_acl *acl_out, uint64_t acl_cap,
                    uint32_t *regions_out, uint64_t regions_cap, uint64_t *acl_n,
-                   uint64_t *regions_n) {
+                   uint64_t *regions_n, int acl_inplace) {
     memset(m, 0, sizeof *m);
     memset(info, 0, sizeof *info);
     *acl_n = 0;
@@ -528,7 +543,7 @@ void oracle_decode(const uint8_t *o, uint64_t len, uint64_t base, honu_meta *m,
     int st = r_bool(&r, &present);                   /* DecodeStruct(meta) :78 */
     if (st == HONU_OK && present) {
         m->present = HONU_HAS_META;
-        st = decode_meta_body(&r, base + t, m, &L);
+        st = decode_meta_body(&r, base + t, m, &L, acl_inplace);
     }
     info->meta_status = st;
     if (st != HONU_OK) {
@@ -582,7 +597,7 @@ int oracle_marshal_batch(const honu_meta *meta, const uint8_t *var, uint64_t var
 int oracle_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint64_t n, honu_meta *meta,
                         honu_record_info *info, honu_acl *acl, uint64_t acl_cap,
                         uint32_t *regions, uint64_t regions_cap, uint8_t *data, uint64_t data_cap,
-                        uint64_t totals[3]) {
+                        uint64_t totals[3], int acl_inplace) {
     uint64_t acl_pos = 0, reg_pos = 0, data_pos = 0;
     int any_cap = 0;
     for (uint64_t i = 0; i < n; i++) {
@@ -592,9 +607,10 @@ int oracle_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
         uint32_t *ro = regions ? regions + (reg_pos < regions_cap ? reg_pos : regions_cap) : NULL;
         uint64_t acap = acl && acl_pos < acl_cap ? acl_cap - acl_pos : 0;
         uint64_t rcap = regions && reg_pos < regions_cap ? regions_cap - reg_pos : 0;
-        oracle_decode(rec + beg, len, beg, &meta[i], &info[i], ao, acap, ro, rcap, &an, &rn);
+        oracle_decode(rec + beg, len, beg, &meta[i], &info[i], ao, acap, ro, rcap, &an, &rn,
+                      acl_inplace);
         if (info[i].meta_status == HONU_OK) {
-            if (meta[i].acl_count) meta[i].acl_off = acl_pos;
+            if (an) meta[i].acl_off = acl_pos;
             if (meta[i].regions_count) meta[i].regions_off = reg_pos;
             if (acl_pos + an > acl_cap || reg_pos + rn > regions_cap) {
                 info[i].meta_status = HONU_ERR_CAPACITY;

@@ -37,9 +37,9 @@ def load():
         "oracle_varint": (C.c_int, [P, U64, P]),
         "oracle_size_bound": (C.c_int64, [C.c_int, P]),
         "oracle_marshal": (C.c_int, [P, P, U64, P, U64, P, U64, P, U64, P, U64, P]),
-        "oracle_decode": (None, [P, U64, U64, P, P, P, U64, P, U64, P, P]),
+        "oracle_decode": (None, [P, U64, U64, P, P, P, U64, P, U64, P, P, C.c_int]),
         "oracle_marshal_batch": (C.c_int, [P, P, U64, P, U64, P, U64, P, P, U64, P, U64, P, P]),
-        "oracle_decode_batch": (C.c_int, [P, P, U64, P, P, P, U64, P, U64, P, U64, P]),
+        "oracle_decode_batch": (C.c_int, [P, P, U64, P, P, P, U64, P, U64, P, U64, P, C.c_int]),
         "oracle_key": (C.c_int, [P, I32, P]),
         "oracle_field_size": (C.c_int64, [U64]),
         "oracle_index_size": (C.c_int64, [P]),
@@ -107,8 +107,13 @@ def marshal_batch(hb):
     return out[:total], out_off, status
 
 
-def decode_batch(rec: np.ndarray, rec_off: np.ndarray, materialize: bool = False):
-    """(meta rows, info, acl table, region table, data arena | None, totals[3])."""
+def decode_batch(rec: np.ndarray, rec_off: np.ndarray, materialize: bool = False,
+                 acl_inplace: bool = True):
+    """(meta rows, info, acl table, region table, data arena | None, totals[3]).
+
+    acl_inplace (the product's default, context param "acl_inplace"): an ACL
+    list whose entries are all present comes back in place (HONU_ACL_INPLACE,
+    acl_off absolute in `rec`), only lists with a nil entry in the table."""
     from honu_amd.metadata import ACL_DTYPE, INFO_DTYPE, META_DTYPE
     lib = load()
     n = len(rec_off) - 1
@@ -125,7 +130,7 @@ def decode_batch(rec: np.ndarray, rec_off: np.ndarray, materialize: bool = False
     totals = np.zeros(3, np.uint64)
     lib.oracle_decode_batch(_p(rec), _p(rec_off), n, _p(meta), _p(info), _p(acl), len(acl),
                             _p(reg), len(reg), _p(data), 0 if data is None else len(data),
-                            _p(totals))
+                            _p(totals), 1 if acl_inplace else 0)
     return (meta[:n], info[:n], acl[: int(totals[0])], reg[: int(totals[1])],
             None if data is None else data[: int(totals[2])], totals)
 
@@ -171,7 +176,8 @@ class CycleWorkspace:
         self._marshal(self.out, self.total)
         self.lib.oracle_decode_batch(_p(self.out), _p(self.out_off), self.n, _p(self.meta),
                                      _p(self.info), _p(self.acl), len(self.acl), _p(self.reg),
-                                     len(self.reg), _p(self.data), len(self.data), _p(self.totals))
+                                     len(self.reg), _p(self.data), len(self.data), _p(self.totals),
+                                     1)  # the product's default ACL form (in place)
         return self.total
 
 

@@ -7,6 +7,10 @@ give for it, as raw little-endian files plus a SHA-256 manifest:
   <name>.records.bin / .offsets.bin   encoded records (CSR, u64 offsets)
   <name>.rows.bin / .info.bin         decoded honu_meta rows / honu_record_info
   <name>.acl.bin / .regions.bin       decoded ACL / region tables
+    (the default form: ACL lists with every entry present returned in place,
+    HONU_ACL_INPLACE; only lists with a nil entry in the ACL table)
+  <name>.rows_table.bin / .acl_table.bin   the same rows / ACL table with every
+    list in the table (context param acl_inplace 0)
 Encode fixtures regenerate their input from the seeded generator (or
 tests/fixtures.py:extreme_metas); decode fixtures carry malformed records.
 
@@ -29,6 +33,8 @@ ENCODE = {  # name -> generator parameters
     "small64": {"seed": 101, "shape": "small", "first": 0, "n": 64},
     "medium8": {"seed": 103, "shape": "medium", "first": 7, "n": 8},
     "extreme40": {"extreme_metas": {"n": 40, "seed": 29}},
+    "large4": {"seed": 105, "shape": "large", "first": 11, "n": 4},
+    "mixed12": {"seed": 106, "shape": "mixed", "first": 3, "n": 12},
 }
 
 
@@ -87,10 +93,13 @@ def outputs(name):
         assert (st == 0).all()
     else:
         rec, off = malformed_records()
-    meta, info, acl, reg, _, tot = oracle.decode_batch(rec, off, False)
+    meta, info, acl, reg, _, tot = oracle.decode_batch(rec, off, False, acl_inplace=True)
+    tmeta, tinfo, tacl, treg, _, ttot = oracle.decode_batch(rec, off, False, acl_inplace=False)
+    assert tinfo.tobytes() == info.tobytes() and treg.tobytes() == reg.tobytes()
     return {"records": rec.tobytes(), "offsets": off.astype("<u8").tobytes(),
             "rows": meta.tobytes(), "info": info.tobytes(), "acl": acl.tobytes(),
-            "regions": reg.astype("<u4").tobytes()}, [int(x) for x in tot]
+            "regions": reg.astype("<u4").tobytes(), "rows_table": tmeta.tobytes(),
+            "acl_table": tacl.tobytes()}, [int(x) for x in tot] + [int(ttot[0])]
 
 
 NAMES = list(ENCODE) + ["malformed"]

@@ -88,7 +88,9 @@ def test_bench_pipeline_bit_exact(oracle_lib, shape, n, after, decode, beside, m
 
 def test_bench_verify_detects_corruption():
     """_verify_chunk (honu_verify_decoded + digests) flags one wrong byte in a
-    decoded ObjectID, span, ACL entry, region or payload."""
+    decoded ObjectID, span, ACL entry (in place in the records arena: its
+    flag, a ClientID byte, its Permissions; or in the table), region or
+    payload."""
     args = bench.parse_args(["--records", "600", "--shape", "small", "--min-chunks", "1"])
     b = bench.Bench(args, 0, 0)
     (a, z), = b.chunks
@@ -113,6 +115,18 @@ def test_bench_verify_detects_corruption():
     assert not flip(sl.dmeta, 352 * i + 96)          # ObjectID byte
     assert not flip(sl.dmeta, 352 * i + 11)          # padding must stay zero
     assert not flip(sl.out, mime)                    # a MIME span byte in the records arena
+    from honu_amd.metadata import ACL_INPLACE
+    pr, acl_off, nacl = (int(rows[i, 0:4].view(np.uint32)[0]), int(rows[i, 320:328].view(np.uint64)[0]),
+                         int(rows[i, 328:336].view(np.uint64)[0]))
+    assert nacl and pr & ACL_INPLACE and int(tot[0]) == 0  # the generator writes no nil entry
+    for k in (0, 1, 17):  # the 2nd entry's flag, a ClientID byte, the Permissions byte
+        assert not flip(sl.out, acl_off + 18 * (nacl // 2) + k)
+    for x in b.slots:  # the table form
+        _lib.check(b.lib.honu_ctx_set_param(x.codec.ctx, b"acl_inplace", 0), "param")
+    sl = b._issue(a, z, False)
+    torch.cuda.synchronize()
+    assert b._verify_chunk(a, z, sl)
+    tot = _host(sl.totals, 24, np.uint64)
     assert not flip(sl.dacl, 20 * (int(tot[0]) // 2) + 3)
     assert not flip(sl.dreg, 4 * (int(tot[1]) // 2))
     info = _host(sl.dinfo, 32 * m, np.uint64).reshape(m, 4)

@@ -243,7 +243,7 @@ def test_feed_acl_table_overflow(oracle_lib):
     HONU_ERR_CAPACITY, acl_n never exceeds the table and acl_needed reports
     what the batch needed; the records before it decode as the oracle says."""
     from honu_amd.feed import RecordFeed
-    from honu_amd.metadata import Metadata, pack_batch
+    from honu_amd.metadata import ACL_INPLACE, Metadata, pack_batch
     flood = Metadata(ACL=[None] * 60000)
     hb = gen_host_batch(5, "small", 0, 4)
     rec, off, _ = oracle_lib.marshal_batch(hb)
@@ -256,7 +256,10 @@ def test_feed_acl_table_overflow(oracle_lib):
         assert feed.append(o) == 0
     res = feed.wait(feed.submit())
     cap = (1 << 17) // 8 + 1024
-    good = sum(int(hb.meta[i]["acl_count"]) for i in range(4))
+    # the generated records' lists have every entry present: returned in
+    # place (HONU_ACL_INPLACE), they take no table entries
+    good = 0
+    assert all(int(res.meta[i]["present"]) & ACL_INPLACE for i in range(4) if res.meta[i]["acl_count"])
     assert res.acl_needed == good + 60000
     assert len(res.acl) == min(res.acl_needed, cap) <= cap
     assert res.info["meta_status"][4] == 9  # HONU_ERR_CAPACITY

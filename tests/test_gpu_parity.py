@@ -21,24 +21,28 @@ from honu_amd.metadata import META_DTYPE, normalize, pack_batch, unpack_row  # n
 from honu_amd.workload import gen_host_batch, gen_meta  # noqa: E402
 
 
-@pytest.fixture(scope="module", params=[(6, 0, 2), (5, 1, 2), (6, 0, 1)], ids=["fused", "split", "fork"])
+@pytest.fixture(scope="module", params=[(6, 2, 1), (5, 0, 1), (6, 1, 1), (6, 2, 0), (5, 2, 0)],
+                ids=["fused", "split", "fork", "fused_table", "split_table"])
 def codec(request):
-    """Both metadata decodes and both header/tail encoders of the product
-    library: the single-launch decode (fused.hip) at every batch size with the
-    default lane encoder + group ACL lists (lane.hip, grp.hip), and the split
-    decode kernels (windowed lane parse, group fill) with the group-layout
-    encoder (enc.hip, encode_variant 1). The default picks the decode by batch
-    size; the bench pipeline and large-batch tests run it. "fork": the ACL
-    lists' kernel placing the lists itself on the context's own stream, beside
-    the lane encoder (encode_fork 1; the default 2 forks only when lane_blocks
-    caps the encoder's grid, as the bench does for large records)."""
+    """Both metadata decodes of the product library with both ACL forms, and
+    both placements of the encoder's ACL lists: the single-launch decode
+    (fused.hip) at every batch size and the split decode kernels (windowed
+    lane parse, group fill); ACL lists returned in place (acl_inplace 1, the
+    default) or every list in the ACL table ("_table"). The default picks the
+    decode by batch size; the bench pipeline and large-batch tests run it.
+    The encoder is the lane encoder + group ACL lists (lane.hip, grp.hip):
+    "split" runs the lists' kernel after the lane encoder (encode_fork 0),
+    "fork" on the context's own stream beside it, placing the lists itself
+    (encode_fork 1; the default 2 forks only when lane_blocks caps the
+    encoder's grid, as the bench does for large records)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     c = hobj.Codec(0, 1 << 18)
-    rv, ev, fork = request.param
+    rv, fork, inplace = request.param
     hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", rv), "param")
-    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"encode_variant", ev), "param")
     hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"encode_fork", fork), "param")
+    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"acl_inplace", inplace), "param")
+    c.acl_inplace = bool(inplace)
     yield c
     c.close()
 
@@ -63,7 +67,8 @@ def gpu_decode(codec, rec, off, materialize=False):
 
 def assert_decode_equal(oracle_lib, codec, rec, off, materialize=False):
     meta, info, acl, reg, data, tot = gpu_decode(codec, rec, off, materialize)
-    ometa, oinfo, oacl, oreg, odata, otot = oracle_lib.decode_batch(rec, off, materialize)
+    ometa, oinfo, oacl, oreg, odata, otot = oracle_lib.decode_batch(
+        rec, off, materialize, getattr(codec, "acl_inplace", True))
     n = len(off) - 1
     assert np.array_equal(tot, otot)
     assert info.tobytes() == oinfo.tobytes()
@@ -183,7 +188,9 @@ def test_decode_capacity(codec, oracle_lib):
                      regions_cap=10, data_cap=4096, rec_bytes=int(off[-1]))
     torch.cuda.synchronize()
     meta, info, acl, reg, data, tot = d.host()
-    assert int(tot[0]) > 10 and int(tot[2]) > 4096
+    # the generator writes no nil ACL entry: in place, no list needs the table
+    assert (int(tot[0]) == 0 if codec.acl_inplace else int(tot[0]) > 10) and int(tot[2]) > 4096
+    assert int(tot[1]) > 10
     assert (info["meta_status"] == 9).any() and (info["data_status"] == 9).any()
     ok = info["data_status"] == 0
     assert (info["data_off"][ok] + info["data_len"][ok] <= 4096).all()
@@ -457,7 +464,7 @@ def test_decode_parse_full_waves(codec, oracle_lib):
     hb = gen_host_batch(23, "small", 0, n)
     rec, off, _ = oracle_lib.marshal_batch(hb)
     meta, info, acl, reg, data, tot = gpu_decode(codec, rec, off)
-    ometa, oinfo, oacl, oreg, odata, otot = oracle_lib.decode_batch(rec, off, False)
+    ometa, oinfo, oacl, oreg, odata, otot = oracle_lib.decode_batch(rec, off, False, codec.acl_inplace)
     assert np.array_equal(tot, otot) and info.tobytes() == oinfo.tobytes()
     assert meta.tobytes() == ometa.tobytes()
     assert acl.tobytes() == oacl.tobytes() and reg.tobytes() == oreg.tobytes()

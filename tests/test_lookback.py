@@ -14,7 +14,11 @@ arrival advances the epoch, resets the ticket and clears misspec; lb_finish is
 the scans' form). Both tile modes advance the same epoch: a test alternates
 them, across an epoch wrap reached by static launches. Then the speculative
 launches' recovery (late-failing records, nil ACL entries, a long unstaged list
-under a capacity failure) and concurrent launches on two streams."""
+under a capacity failure) and concurrent launches on two streams. The
+speculation and tile tests run with both ACL forms (context param
+acl_inplace: lists with every entry present returned in place, the default,
+whose speculated flags the launch gathers after its publish; or every list in
+the table, whose flags the table fill checks)."""
 import numpy as np
 import pytest
 
@@ -26,6 +30,11 @@ from honu_amd import object as hobj  # noqa: E402
 from honu_amd.workload import gen_host_batch  # noqa: E402
 
 EPOCHS = 1 << 18
+FORMS = pytest.mark.parametrize("inplace", [1, 0], ids=["acl_inplace", "acl_table"])
+
+
+def _form(c, inplace):
+    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"acl_inplace", inplace), "param")
 
 
 def _dev(a, codec):
@@ -35,8 +44,9 @@ def _dev(a, codec):
 class _Dec:
     """Preallocated honu_decode_records over one encoded batch."""
 
-    def __init__(self, codec, rec, off):
+    def __init__(self, codec, rec, off, inplace=1):
         self.c, self.n = codec, len(off) - 1
+        self.inplace = inplace
         self.rec, self.off = _dev(rec, codec), _dev(off, codec)
         cap = int(off[-1])
         self.acl_cap = self.reg_cap = cap
@@ -46,6 +56,7 @@ class _Dec:
 
     def __call__(self):
         L = hobj._lib
+        _form(self.c, self.inplace)
         return self.c.lib.honu_decode_records(
             self.c.ctx, L.ptr(self.rec), L.ptr(self.off), self.n, L.ptr(self.meta),
             L.ptr(self.info), L.ptr(self.acl), self.acl_cap, L.ptr(self.reg), self.reg_cap, 0, 0,
@@ -53,7 +64,7 @@ class _Dec:
 
     def check(self, oracle_lib, rec, off):
         torch.cuda.synchronize()
-        ometa, oinfo, oacl, oreg, _, otot = oracle_lib.decode_batch(rec, off, False)
+        ometa, oinfo, oacl, oreg, _, otot = oracle_lib.decode_batch(rec, off, False, bool(self.inplace))
         tot = self.tot[:24].cpu().numpy().view(np.uint64)
         assert np.array_equal(tot, otot)
         assert self.meta[:352 * self.n].cpu().numpy().tobytes() == ometa.tobytes()
@@ -71,11 +82,12 @@ def codec():
     c.close()
 
 
-def test_tile_counts(codec, oracle_lib):
+@FORMS
+def test_tile_counts(codec, oracle_lib, inplace):
     for tiles, seed in ((1, 1), (2, 2), (3, 3), (65, 4), (66, 5), (129, 6), (300, 7)):
         n = 64 * tiles - (seed % 3) * 7  # ragged last tile too
         rec, off, _ = oracle_lib.marshal_batch(gen_host_batch(seed, "small", 0, n))
-        d = _Dec(codec, rec, off)
+        d = _Dec(codec, rec, off, inplace)
         assert d() == 0
         d.check(oracle_lib, rec, off)
 
@@ -155,9 +167,10 @@ def test_static_tiles_beside_a_copy_that_fills_the_chip(oracle_lib):
         c.close()
 
 
+@FORMS
 @pytest.mark.parametrize("n,bad", [(140000, [77]), (140000, [5, 64 * 1500 + 3, 139999]),
                                    (5000, [1234])])
-def test_speculative_publish_recovers(oracle_lib, n, bad):
+def test_speculative_publish_recovers(oracle_lib, n, bad, inplace):
     """Launches with more tiles than resident waves (here 2188 tiles) publish a
     tile's counts once its regions are read (fused.hip SpecPub). Records
     truncated by a few bytes fail in a later field (the Modified time), so
@@ -180,23 +193,25 @@ def test_speculative_publish_recovers(oracle_lib, n, bad):
     c = hobj.Codec(0, n)
     try:
         hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
-        d = _Dec(c, brec, boff)
+        d = _Dec(c, brec, boff, inplace)
         assert d() == 0
         d.check(oracle_lib, brec, boff)
         info = d.info[:32 * n].cpu().numpy().view(np.int32).reshape(n, 8)
         assert all(info[i, 5] != 0 for i in bad)  # meta_status of the truncated records
-        good = _Dec(c, rec, off)
+        good = _Dec(c, rec, off, inplace)
         assert good() == 0
         good.check(oracle_lib, rec, off)
     finally:
         c.close()
 
 
+@FORMS
 @pytest.mark.parametrize("n,k", [(140000, 1), (140000, 200)])
-def test_speculative_acl_flags_recover(oracle_lib, n, k):
+def test_speculative_acl_flags_recover(oracle_lib, n, k, inplace):
     """Speculative launches also take every ACL list that fits its record as
-    all present without gathering its entry flags (fused.hip FUSED_SPEC_ACL);
-    the table fill checks them. Records whose lists hold nil entries (the walk
+    all present without gathering its entry flags in the walk; the table fill
+    (table form) or the flag gather after the publish (in-place form, fused.hip
+    flag_gather / flag_check) checks them. Records whose lists hold nil entries (the walk
     then read every later field at the wrong place) are spliced into a
     2188-tile batch: the fill must raise misspec and the guarded launch redo
     the batch bit-exact with the oracle; a clean batch decoded next on the same
@@ -227,14 +242,23 @@ def test_speculative_acl_flags_recover(oracle_lib, n, k):
     c = hobj.Codec(0, n)
     try:
         hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
-        d = _Dec(c, brec, boff)
+        r0 = _get(c, b"recoveries")
+        d = _Dec(c, brec, boff, inplace)
         assert d() == 0
         d.check(oracle_lib, brec, boff)
-        good = _Dec(c, rec, off)
+        assert _get(c, b"recoveries") == r0 + 1  # the guarded launch redid the batch
+        good = _Dec(c, rec, off, inplace)
         assert good() == 0
         good.check(oracle_lib, rec, off)
     finally:
         c.close()
+
+
+def _get(c, name):
+    import ctypes as C
+    v = C.c_int64(-1)
+    hobj._lib.check(c.lib.honu_ctx_get_param(c.ctx, name, C.byref(v)), "get_param")
+    return v.value
 
 
 def test_speculation_backs_off_after_a_recovery(oracle_lib):
@@ -325,7 +349,8 @@ def test_concurrent_ticket_and_static_launches_on_two_streams(oracle_lib):
         c2.close()
 
 
-def test_speculated_long_list_checked_under_capacity_failure(oracle_lib):
+@FORMS
+def test_speculated_long_list_checked_under_capacity_failure(oracle_lib, inplace):
     """A speculated ACL list too long to be staged (1,200 entries: more than
     STAGE_SLOTS blocks) whose last entry is nil, in the last record of a
     2188-tile batch, with acl_cap one entry short of the batch's total so that
@@ -349,13 +374,13 @@ def test_speculated_long_list_checked_under_capacity_failure(oracle_lib):
     assert r2[-7:].tobytes() == bytes(7)  # last region 0, then six zero bytes
     brec = np.concatenate([rec, r2])
     boff = np.concatenate([off, off[-1] + o2[1:]]).astype(np.uint64)
-    ometa, oinfo, oacl, oreg, _, otot = oracle_lib.decode_batch(brec, boff, False)
+    ometa, oinfo, oacl, oreg, _, otot = oracle_lib.decode_batch(brec, boff, False, bool(inplace))
     assert int(ometa[-1]["regions_count"]) == 5 and int(ometa[-1]["acl_count"]) == 1200
     acl_cap, reg_cap = int(otot[0]) - 1, int(otot[1]) + 16
     c = hobj.Codec(0, n)
     try:
         hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
-        d = _Dec(c, brec, boff)
+        d = _Dec(c, brec, boff, inplace)
         d.acl_cap, d.reg_cap = acl_cap, reg_cap
         assert d() == 0
         torch.cuda.synchronize()
