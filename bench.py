@@ -112,6 +112,10 @@ def parse_args(argv=None):
                    help="encdec mode, comma list of extra legs after the main one: small (1M Small "
                         "encode + decode, configs[1]), mixed_encode (1M Mixed encode, configs[3]); "
                         "auto: both for the default Large line, none otherwise; none: no legs")
+    p.add_argument("--decode-prio", type=int, default=0, choices=[0, 1],
+                   help="1: a chunk's single-launch decode (and its guarded launch) on a high-priority "
+                        "stream of its slot, so the guard's workgroups are dispatched before the other "
+                        "slot's metadata kernels when CUs free up")
     p.add_argument("--decode-chain", type=int, default=1, choices=[0, 1],
                    help="with two metadata streams, a chunk's single-launch decode waits for the "
                         "previous chunk's (and its guarded launch): the guard never queues for "
@@ -260,6 +264,9 @@ class Bench:
         self.sd = self.sc
         if getattr(args, "copy_streams", 1) == 2 and nslots == 2 and not args.meta_cu_stride:
             self.sd = torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio > 0 else 0)
+        # --decode-prio: one high-priority decode stream per metadata stream
+        self.sdec = [torch.cuda.Stream(self.dev, priority=-1) for _ in self.sms] \
+            if getattr(args, "decode_prio", 0) else None
         self.sv = torch.cuda.Stream(self.dev)  # verification of drained chunks
         self.events = None
         self.last = None
@@ -304,7 +311,7 @@ class Bench:
             ok &= self._check(check, pending)
         torch.cuda.current_stream(self.dev).wait_stream(self.sc)
         torch.cuda.current_stream(self.dev).wait_stream(self.sd)
-        for sm in self.sms:
+        for sm in self.sms + (self.sdec or []):
             torch.cuda.current_stream(self.dev).wait_stream(sm)
         return ok
 
@@ -354,15 +361,25 @@ class Bench:
             # otherwise wait up to ~1 ms for LDS this decode's persistent grid
             # holds, and hold up its stream meanwhile
             chain = self.args.decode_chain and len(self.sms) > 1
+            dm = sm
+            if self.sdec is not None:  # fork onto the slot's high-priority decode stream
+                dm = self.sdec[k % len(self.sdec)]
+                ev = torch.cuda.Event()
+                ev.record(sm)
+                dm.wait_event(ev)
             if chain and self.dec_done is not None:
-                sm.wait_event(self.dec_done)
+                dm.wait_event(self.dec_done)
             _lib.check(L.honu_decode_records(c, P(sl.out), P(sl.out_off), n, P(sl.dmeta),
                                              P(sl.dinfo), P(sl.dacl), self.acl_cap, P(sl.dreg),
-                                             self.reg_cap, 1, self.data_cap, P(sl.totals), ms),
+                                             self.reg_cap, 1, self.data_cap, P(sl.totals), dm.cuda_stream),
                        "decode_records")
             if chain:
                 self.dec_done = torch.cuda.Event()
-                self.dec_done.record(sm)
+                self.dec_done.record(dm)
+            if dm is not sm:  # join: the fill event below and the slot's next chunk follow it
+                ev = torch.cuda.Event()
+                ev.record(dm)
+                sm.wait_event(ev)
         else:
             _lib.check(L.honu_decode_parse(c, P(sl.out), P(sl.out_off), n, P(sl.dmeta),
                                            P(sl.dinfo), ms), "decode_parse")

@@ -29,6 +29,7 @@
 #include <string.h>
 
 #include "../include/honu_codec.h"
+#include "../include/honu_bench.h" /* the synthetic batch and the digest */
 
 #define CHECK(x)                                                                          \
     do {                                                                                  \

@@ -85,6 +85,24 @@ static int fused_blocks(const LaunchGeom &g) {
     return g.lane_blocks > 0 && g.lane_blocks < resident ? g.lane_blocks : resident;
 }
 
+// A stream with a CU mask or a non-default priority: honu_encode_records then
+// does not fork the ACL lists onto the context's own (unmasked, default
+// priority) stream, so the work stays where the caller put it.
+static bool stream_is_restricted(hipStream_t s, int num_cu) {
+    int prio = 0;
+    if (hipStreamGetPriority(s, &prio) == hipSuccess && prio != 0) return true;
+    uint32_t mask[32] = {0};
+    const uint32_t words = (uint32_t)((num_cu + 31) / 32);
+    if (words > 32 || hipExtStreamGetCUMask(s, words, mask) != hipSuccess) return false;
+    bool any = false, all = true;  // (an all-zero answer: no mask)
+    for (int i = 0; i < num_cu; i++) {
+        const bool on = mask[i / 32] >> (i % 32) & 1u;
+        any |= on;
+        all &= on;
+    }
+    return any && !all;
+}
+
 static int env_int(const char *name, int dflt) {
     const char *v = getenv(name);
     return v && *v ? atoi(v) : dflt;
@@ -358,7 +376,11 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
     // with the ACL lists' partial end chunks (one record per lane), then the
     // lists' whole chunks (16 lanes per record)
     hipStream_t s = (hipStream_t)stream;
-    const bool fork = ctx->enc_fork == 1 || (ctx->enc_fork == 2 && ctx->geom.lane_blocks > 0);
+    // (auto: not on a CU-masked or prioritised caller stream, whose placement
+    // the fork would escape)
+    const bool fork = ctx->enc_fork == 1 ||
+                      (ctx->enc_fork == 2 && ctx->geom.lane_blocks > 0 && n &&
+                       !stream_is_restricted(s, ctx->geom.num_cu));
     if (fork && n) {
         // the lists' whole chunks on the context's own stream, beside the
         // header/tail encoder (disjoint bytes: the lane encoder writes the
@@ -370,13 +392,13 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
         HIPCHK(hipEventRecord(ctx->ev_join, ctx->aux));
         HIPCHK(launch_encode_meta_lane(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
                                        out_cap, d_out_off, d_status, ctx->enc_acl,
-                                       ctx->geom.lane_blocks, s));
+                                       ctx->geom.lane_blocks, ctx->geom.num_cu, s));
         HIPCHK(hipStreamWaitEvent(s, ctx->ev_join, 0));
         return HONU_OK;
     }
     HIPCHK(launch_encode_meta_lane(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
                                    out_cap, d_out_off, d_status, ctx->enc_acl,
-                                   ctx->geom.lane_blocks, s));
+                                   ctx->geom.lane_blocks, ctx->geom.num_cu, s));
     HIPCHK(launch_encode_acl_grp(d_meta, d_acl, n, d_out, d_status, ctx->enc_acl,
                                  ctx->geom.lane_blocks, s));
     return HONU_OK;

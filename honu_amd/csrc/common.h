@@ -9,6 +9,7 @@
 #include <stdint.h>
 
 #include "../../include/honu_codec.h"
+#include "../../include/honu_bench.h"
 
 #define HONU_WAVE 64
 #define HONU_BLOCK 256

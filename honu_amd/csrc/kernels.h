@@ -113,7 +113,8 @@ hipError_t launch_decode_keys(const LaunchGeom &g, const honu_meta *meta,
 hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
                                    const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
                                    uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
-                                   int32_t *status, uint64_t *acl_out, int max_blocks, hipStream_t s);
+                                   int32_t *status, uint64_t *acl_out, int max_blocks, int num_cu,
+                                   hipStream_t s);
 hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uint64_t n,
                                  uint8_t *out, const int32_t *status, const uint64_t *acl_pos,
                                  int max_blocks, hipStream_t s);

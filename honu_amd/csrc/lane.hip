@@ -22,10 +22,10 @@ namespace honu {
 // Small 0.298 -> 0.265 ms; 64 K Small 0.074 -> 0.078 ms and a 62 K Large chunk
 // 0.082 -> 0.086 ms (latency-bound: fewer records in flight per SIMD and
 // lines held back lengthen a tile), hence the switch.
-#ifndef ENC_LINE_MIN_TILES_N  // (A/B builds only)
-#define ENC_LINE_MIN_TILES_N (2 * 4 * 256)  // the line form's resident waves (2 workgroups x 4 waves x 256 CUs)
-#endif
-constexpr uint64_t ENC_LINE_MIN_TILES = ENC_LINE_MIN_TILES_N;
+// The switch: more tiles than the line form's resident waves, i.e. 4 waves x
+// min(the launch's workgroups, 2 per CU) (launch_encode_meta_lane; a
+// lane_blocks cap lowers it). ENC_LINE_MIN_TILES_N fixes it instead (A/B
+// builds only).
 template <int RING> constexpr uint32_t enc_wave_bytes() { return (RING > 0 ? RING : 1) * HONU_WAVE * 16; }
 
 template <bool SKIP_ACL, int RING>
@@ -197,14 +197,23 @@ static dim3 lane_grid(uint64_t n, int cap) {
 hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
                                    const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
                                    uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
-                                   int32_t *status, uint64_t *acl_out, int max_blocks, hipStream_t s) {
+                                   int32_t *status, uint64_t *acl_out, int max_blocks, int num_cu,
+                                   hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (!acl_out) return hipErrorInvalidValue;
-    if ((n + HONU_WAVE - 1) / HONU_WAVE > ENC_LINE_MIN_TILES)
-        hipLaunchKernelGGL((k_encode_meta_lane<true, 16>), lane_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta,
+    const dim3 grid = lane_grid(n, max_blocks);
+#ifdef ENC_LINE_MIN_TILES_N
+    const uint64_t line_min_tiles = ENC_LINE_MIN_TILES_N;
+    (void)num_cu;
+#else
+    const uint64_t resident_blocks = grid.x < 2u * (uint64_t)num_cu ? grid.x : 2u * (uint64_t)num_cu;
+    const uint64_t line_min_tiles = HONU_WAVES_PER_BLOCK * resident_blocks;
+#endif
+    if ((n + HONU_WAVE - 1) / HONU_WAVE > line_min_tiles)
+        hipLaunchKernelGGL((k_encode_meta_lane<true, 16>), grid, dim3(HONU_BLOCK), 0, s, meta,
                            var, acl, reg, payload_off, n, out, out_cap, out_off, status, acl_out);
     else
-        hipLaunchKernelGGL((k_encode_meta_lane<true, 8>), lane_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta,
+        hipLaunchKernelGGL((k_encode_meta_lane<true, 8>), grid, dim3(HONU_BLOCK), 0, s, meta,
                            var, acl, reg, payload_off, n, out, out_cap, out_off, status, acl_out);
     return hipGetLastError();
 }

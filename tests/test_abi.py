@@ -1,5 +1,7 @@
-"""The C-ABI library loads on a CPU-only host, exports every symbol the header
-declares, and its struct layouts match the host-side numpy views."""
+"""The C-ABI library loads on a CPU-only host, exports every symbol the headers
+declare (include/honu_codec.h: the drop-in boundary; include/honu_bench.h:
+the generator, digests, verifier and probe the bench and tests use), and its
+struct layouts match the host-side numpy views."""
 import os
 import re
 import subprocess
@@ -13,12 +15,15 @@ from honu_amd.system import COLLECTION_DTYPE, INDEX_DTYPE
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "honu_codec.h")
+BENCH_HEADER = os.path.join(ROOT, "include", "honu_bench.h")
 
 
-def header_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(honu_[a-z0-9_]+)\s*\(", src)))
+def header_functions(paths=(HEADER, BENCH_HEADER)):
+    names = set()
+    for path in paths:
+        src = re.sub(r"/\*.*?\*/", "", open(path).read(), flags=re.S)
+        names |= set(re.findall(r"\b(honu_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():
@@ -28,6 +33,15 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
     assert set(names) == set(_lib.EXPORTS)
+
+
+def test_product_header_is_the_binding():
+    """The product header holds what INTEGRATION.md binds; the measurement
+    entry points live in honu_bench.h only."""
+    product = set(header_functions((HEADER,)))
+    bench_only = set(header_functions((BENCH_HEADER,))) - product
+    assert {"honu_gen_meta", "honu_digest_records", "honu_verify_decoded", "honu_hbm_probe"} <= bench_only
+    assert not product & {"honu_gen_totals", "honu_gen_payload", "honu_digest_host"}
 
 
 STRUCTS = ((META_DTYPE, "honu_meta"), (ACL_DTYPE, "honu_acl"), (INFO_DTYPE, "honu_record_info"),

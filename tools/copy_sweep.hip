@@ -3,7 +3,8 @@
 // MI355X_MICROARCH.md "Chip-level parameters", and which form does).
 // Standalone measurement tool, not product code:
 //   hipcc -O3 --offload-arch=gfx950 -o copy_sweep tools/copy_sweep.hip
-//   ./copy_sweep [GiB per buffer, default 8] [reps, default 5]
+//   ./copy_sweep [GiB per buffer, default 8] [reps, default 5] [read|write|copy]
+// (the third argument: that one form only, for rocprofv3 --pmc passes)
 // Swept: 16/32/64 B per lane, 1-16 chunks per lane in flight, each wave on a
 // contiguous range (the codec copy engine's layout, copy.hip) or grid-stride
 // (the guide's float4 copy), global_load/store or buffer_load/store with the
@@ -14,6 +15,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <stdint.h>
+#include <string.h>
 #include <vector>
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -173,6 +175,20 @@ int main(int argc, char **argv) {
                name, bpc, ms, traffic / (ms * 1e-3) / 1e12, extra);
         fflush(stdout);
     };
+    // "only": one form, reps launches, for counter passes (rocprofv3 --pmc)
+    const char *only = argc > 3 ? argv[3] : nullptr;
+    if (only) {
+        const dim3 g(cus * 2);
+        float ms = 0;
+        if (!strcmp(only, "read"))
+            ms = time([&] { hipLaunchKernelGGL(k_read, g, dim3(256), 0, 0, a, n, o); });
+        else if (!strcmp(only, "write"))
+            ms = time([&] { hipLaunchKernelGGL(k_write, g, dim3(256), 0, 0, b, n); });
+        else
+            ms = time([&] { launch_copy<1, 8, L_RANGE, M_GLOBAL, 0, 0>(g, a, b, n); });
+        line(only, "range_16B_u8", 2, (strcmp(only, "copy") ? 1.0 : 2.0) * bytes, ms, "");
+        return 0;
+    }
     const int bpcs[] = {1, 2, 3, 4, 6, 8};
     for (int bpc : bpcs) {
         const dim3 g(cus * bpc);
