@@ -970,9 +970,10 @@ def hbm_probe(codec, dev, nbytes=4 << 30, reps=5):
     """The part's achievable streaming rates, measured in this process with the
     library's own probe kernels (honu_hbm_probe: 16 B per lane, the layout of
     tools/hbm_probe.hip and of the guide's float4 copy): read-only, write-only
-    and copy (per-wave ranges and grid-stride, 1/2/4 workgroups per CU; the
-    best copy is `copy_gbs`, the roofline's achievable denominator). Copy rates
-    count read + write bytes."""
+    and copy (per-wave ranges, grid-stride and per-wave ranges with
+    non-temporal loads and stores, 1/2/4 workgroups per CU; the best copy is
+    `copy_gbs`, the roofline's achievable denominator). Copy rates count read +
+    write bytes."""
     from honu_amd import _lib
     L, c = codec.lib, codec.ctx
     s = torch.cuda.current_stream(dev).cuda_stream
@@ -997,9 +998,9 @@ def hbm_probe(codec, dev, nbytes=4 << 30, reps=5):
     out = {"bytes": nbytes, "reps": reps}
     out["read_gbs"] = max(rate(0, k) for k in (1, 2, 4))
     out["write_gbs"] = max(rate(1, k) for k in (1, 2, 4))
-    best = max(((rate(m, k), m, k) for m in (2, 3) for k in (1, 2, 4)), key=lambda x: x[0])
-    out["copy_gbs"], out["copy_form"] = best[0], (
-        f"{'wave ranges' if best[1] == 2 else 'grid stride'}, {best[2]} workgroups per CU")
+    forms = {2: "wave ranges", 3: "grid stride", 4: "wave ranges, non-temporal"}
+    best = max(((rate(m, k), m, k) for m in (2, 3, 4) for k in (1, 2, 4)), key=lambda x: x[0])
+    out["copy_gbs"], out["copy_form"] = best[0], f"{forms[best[1]]}, {best[2]} workgroups per CU"
     del a, b
     torch.cuda.empty_cache()
     return out

@@ -45,6 +45,8 @@ struct honu_ctx {
     hipEvent_t ev_fork, ev_join;
     int enc_fork;            // honu_ctx_set_param("encode_fork", 0 off / 1 on / 2 auto: when lane_blocks caps the grid)
     bool acl_inplace;        // honu_ctx_set_param("acl_inplace"): decode returns all-present ACL lists in place
+    bool inline_recovery;    // honu_ctx_set_param("inline_recovery"): ticket-form launches recover in-launch
+    int guard_blocks;        // honu_ctx_set_param("guard_blocks"): workgroups of the guarded launch (0: full grid)
 };
 static constexpr uint32_t SPEC_BACKOFF_CALLS = 16;
 
@@ -191,6 +193,12 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     if (c->geom.record_variant != 5 && c->geom.record_variant != 6)
         c->geom.record_variant = 0;
     c->acl_inplace = env_int("HONU_ACL_INPLACE", 1) != 0;
+    // measured slower than the guarded launch (1M Small zero copy 0.56 ->
+    // 0.67-0.70 ms, the Small step 4.17-4.21 -> 4.26-4.42 ms; DESIGN §3
+    // "Round 5"): off by default
+    c->inline_recovery = env_int("HONU_INLINE_RECOVERY", 0) != 0;
+    c->guard_blocks = env_int("HONU_GUARD_BLOCKS", 0);
+    if (c->guard_blocks < 0) c->guard_blocks = 0;
     const uint64_t n = c->max_n;
     const uint64_t np = 0;
     const uint64_t map_cap = HONU_AB_BUILD ? 1ull << 22 : 0;  // tile map (A/B sweep copy)
@@ -293,6 +301,8 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
     else if (!strcmp(name, "speculate") && (value == 0 || value == 1)) ctx->spec_allowed = value != 0;
     else if (!strcmp(name, "encode_fork") && value >= 0 && value <= 2) ctx->enc_fork = (int)value;
     else if (!strcmp(name, "acl_inplace") && (value == 0 || value == 1)) ctx->acl_inplace = value != 0;
+    else if (!strcmp(name, "inline_recovery") && (value == 0 || value == 1)) ctx->inline_recovery = value != 0;
+    else if (!strcmp(name, "guard_blocks") && value >= 0 && value <= 65536) ctx->guard_blocks = (int)value;
     else if (!strcmp(name, "speculate_backoff") && value >= 0 && value <= (int64_t)SPEC_BACKOFF_CALLS) {
         __atomic_store_n(ctx->spec_seen, 0u, __ATOMIC_RELAXED);
         ctx->spec_off = (uint32_t)value;
@@ -316,6 +326,8 @@ int32_t honu_ctx_get_param(const honu_ctx *ctx, const char *name, int64_t *value
     else if (!strcmp(name, "speculate")) *value = ctx->spec_allowed ? 1 : 0;
     else if (!strcmp(name, "encode_fork")) *value = ctx->enc_fork;
     else if (!strcmp(name, "acl_inplace")) *value = ctx->acl_inplace ? 1 : 0;
+    else if (!strcmp(name, "inline_recovery")) *value = ctx->inline_recovery ? 1 : 0;
+    else if (!strcmp(name, "guard_blocks")) *value = ctx->guard_blocks;
     else if (!strcmp(name, "recoveries"))  // recovery launches that ran, since the context was created
         *value = __atomic_load_n(ctx->spec_seen + 1, __ATOMIC_RELAXED);
     else if (!strcmp(name, "speculate_backoff"))  // calls the next call starts without speculation
@@ -539,7 +551,8 @@ int32_t honu_decode_records(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t 
                                regions_cap, materialize != 0, data_cap, ctx->scratch, ctx->offs,
                                tot, ctx->lb_dec, ctx->lb_dec_status, ctx->lb_dec_gstatus,
                                ctx->lb_dec_words, fused_blocks(ctx->geom), ctx->spec_seen,
-                               ctx->spec_seen + 1, spec, ctx->acl_inplace, s));
+                               ctx->spec_seen + 1, spec, ctx->acl_inplace, ctx->inline_recovery,
+                               ctx->guard_blocks, s));
     return HONU_OK;
 }
 
@@ -736,7 +749,7 @@ int32_t honu_gen_payload(honu_ctx *ctx, uint64_t seed, uint64_t first, uint64_t 
 int32_t honu_hbm_probe(honu_ctx *ctx, int32_t mode, const void *d_src, void *d_dst, uint64_t bytes,
                        uint32_t blocks_per_cu, void *stream) {
     if (!ctx) return arg_fail("ctx");
-    if (mode < 0 || mode > 3) return arg_fail("mode");
+    if (mode < 0 || mode > 4) return arg_fail("mode");
     if (!aligned(d_src, 16) || !aligned(d_dst, 16) || (mode != 1 && !d_src) || (mode != 0 && !d_dst))
         return arg_fail("buffers must be non-null and 16-byte aligned");
     if (!blocks_per_cu) blocks_per_cu = 2;

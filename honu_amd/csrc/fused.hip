@@ -80,6 +80,7 @@ static_assert(STAGE_SLOTS % HONU_WAVE == 0, "whole instructions");
 // parity green, 62 K Large 0.076-0.080 vs 0.077-0.080 ms, 64 K / 40 K / 16 K
 // Small equal, profiles/r04/ab/dec_pair_fill_ab.jsonl.)
 enum { FORM_TICKET = 0, FORM_STATIC = 1 };
+template <bool B> struct BoolC { static constexpr bool value = B; };
 template <int FORM> constexpr uint32_t form_slots() { return STAGE_SLOTS; }
 // a wave's LDS: its windows during the walk, the staging after it
 template <int FORM> constexpr uint32_t form_wave_bytes() {
@@ -309,11 +310,29 @@ struct SpecPub {
 // tiles and grouped prefixes instead of tickets and the look-back over group
 // totals (lookback.h); each form a kernel of its own, so none pays another's
 // registers or LDS.
+//
+// In-launch recovery (ticket form, MODE 1 with `inline_rec`): instead of a
+// guarded second launch, the speculative launch itself finishes the job. A
+// wave whose ticket loop ends counts its tiles into LbState::tdone and waits
+// until every tile of the pass is counted (the tiles it waits for are held
+// by running waves: tickets are only taken by running waves, so this cannot
+// deadlock, also when the grid is not resident at once); misspec is final
+// then. Clean (the usual case): the wave ends. Misspeculated: every wave
+// releases its stores (agent scope: the pass-1 stores of the same outputs,
+// maybe from another XCD, must land after them), counts its tiles into
+// rdone, and once all are released the waves decode the batch again without
+// speculation from a second ticket counter, with look-back words tagged as
+// pass 1 (lookback.h). No launch waits for a CU with 78 KB of free LDS
+// behind other kernels (a guard launch that was a no-op
+// spent up to 1.4 ms queued beside the bench's copies and encoder). Static
+// tiles keep the guarded launch: their waves may wait on workgroups that are
+// not resident yet, so a launch-wide wait could deadlock beside another
+// persistent kernel.
 template <int MODE, int FORM, bool INPL>
 __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
     DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t *lb_gstatus, uint64_t lb_words,
-    uint32_t *spec_seen, uint32_t *recoveries) {
+    uint32_t *spec_seen, uint32_t *recoveries, bool inline_rec) {
     constexpr int mode = MODE;
     if (mode == 2 && __hip_atomic_load(&lb->misspec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
         return;  // every wave of the launch returns: the look-back state is untouched
@@ -333,6 +352,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     const uint32_t lane = lane_id();
     const uint32_t ep = lb_epoch(lb);
     const uint64_t ntiles = (n + HONU_WAVE - 1) / HONU_WAVE;
+    const bool ir = MODE == 1 && FORM == FORM_TICKET && inline_rec;  // in-launch recovery
     const uint64_t waves = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
     // every tile has a resident wave of its own: static tiles (lookback.h)
     // (measured: taking the next ticket and loading its bounds before the
@@ -359,6 +379,13 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         tk = wg_ticket + threadIdx.x / HONU_WAVE;
         tk_pending = true;
     }
+    uint32_t my_tiles = 0;  // tiles of pass 0 this wave decoded
+    // one pass over the tiles; SPEC (compile time): speculative publish and
+    // ACL flags (mode 1's first pass), so each pass is specialised
+    auto tiles = [&](auto spec_c, uint32_t pass) {
+    constexpr bool spec = decltype(spec_c)::value;
+    const uint32_t tag = pass ? (ep | LB_PASS_BIT) : ep;  // look-back words of this pass
+    uint32_t *tctr = pass ? &lb->ticket2 : &lb->ticket;
     for (;;) {
         uint64_t t;
         if constexpr (stat_idx) {
@@ -368,9 +395,15 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
             t = __builtin_amdgcn_readlane(tk, 0);
             tk_pending = false;
         } else {
-            t = lb_ticket(lb);
+            t = lb_ticket(tctr);
         }
         if (t >= ntiles) break;
+        if (pass == 0) my_tiles++;
+        // the recovery pass tells the host (once: the wave holding its first tile)
+        if (pass == 1 && t == 0 && spec_seen && lane == 0) {
+            __hip_atomic_store(spec_seen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (recoveries) __hip_atomic_fetch_add(recoveries, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         const uint64_t i0 = t * HONU_WAVE, i = i0 + lane;
         const uint64_t lim = i0 + HONU_WAVE < n ? i0 + HONU_WAVE : n;  // the tile's records are [i0, lim)
         const bool valid = i < lim;
@@ -380,11 +413,11 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         WinParse P;
         RegRow R;
         SpecPub early;
-        early.on = mode == 1;
+        early.on = spec;
         early.spec_acl = early.on;
         early.status = lb_status;
         early.t = t;
-        early.ep = ep;
+        early.ep = tag;
         win_walk(i0, ws, rec, lim, H, R, P, early, INPL);
 
         // counts -> offsets: wave scan + look-back across tiles
@@ -405,7 +438,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
             x2 = wave_excl(c2, agg[2]);
             // publish, then write the rows while the predecessors finish
             // (their list offsets are patched in below)
-            lb_publish<3>(lb_status, t, ep, agg);
+            lb_publish<3>(lb_status, t, tag, agg);
         }
         rows_out<true>(ws, R, i0, lim, O.meta);
         // table form (acl_inplace 0): the ACL lists with every entry present
@@ -427,15 +460,15 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
         if (igather) flag_gather(ws, rec, ichk ? (P.acl_pos & GRP_POS_MASK) : 0, ichk ? P.nacl : 0, 0);
         WSTAMP(10);  // publish + rows out + first staging round issued
         if constexpr (STAT)  // every tile runs at once: grouped prefixes (lookback.h)
-            lb_resolve_grouped<3>(lb_status, lb_gstatus, t, ntiles, ep, agg, excl);
+            lb_resolve_grouped<3>(lb_status, lb_gstatus, t, ntiles, tag, agg, excl);
         else  // tickets: a decoupled look-back over the group totals (the plain
               // one over tile words, lb_resolve, measured 3 % slower on 1M Small)
-            lb_resolve_grouped_lb<3>(lb_status, lb_gstatus, t, ntiles, ep, agg, excl);
+            lb_resolve_grouped_lb<3>(lb_status, lb_gstatus, t, ntiles, tag, agg, excl);
         WSTAMP(11);  // look-back wait
         // nothing is staged in the in-place form: the next ticket is requested
         // here, and the rest of the tile hides its round trip
         if (!stat_idx && igather) {
-            tk = lb_ticket_issue(lb);
+            tk = lb_ticket_issue(tctr);
             tk_pending = true;
         }
         if (t == ntiles - 1 && lane < 3)
@@ -530,7 +563,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
             const bool last = S.stop >= S.nbtot;  // wave-uniform
             acl_bad |= S.store(ws, O.acl, ao, ok, early.spec_acl, [&]() {
                 if (last && !stat_idx) {
-                    tk = lb_ticket_issue(lb);
+                    tk = lb_ticket_issue(tctr);
                     tk_pending = true;
                 }
             });
@@ -547,8 +580,31 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
             __hip_atomic_store(&lb->misspec, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         WSTAMP(13);  // ACL fill
     }
+    };  // tiles
+    tiles(BoolC<MODE == 1>{}, 0u);
+    if constexpr (MODE == 1 && FORM == FORM_TICKET) {
+        if (ir) {
+            // in-launch recovery (above): the speculative pass is over for
+            // this wave; its misspec store (sc1) has completed before its
+            // tiles are counted
+            __builtin_amdgcn_s_waitcnt(0);
+            if (lane == 0) __hip_atomic_fetch_add(&lb->tdone, my_tiles, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lb_wait_count(&lb->tdone, ntiles);
+            uint32_t ms = 0;
+            if (lane == 0) ms = __hip_atomic_load(&lb->misspec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__builtin_amdgcn_readlane(ms, 0)) {  // misspeculated (else: done)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // pass-0 stores reach memory
+                if (lane == 0)
+                    __hip_atomic_fetch_add(&lb->rdone, my_tiles, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                lb_wait_count(&lb->rdone, ntiles);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                tk_pending = false;
+                tiles(BoolC<false>{}, 1u);
+            }
+        }
+    }
     WSTAMP_FLUSH();
-    lb_finish_blocks(lb, lb_status, lb_words, gridDim.x, &last_flag, mode == 2);
+    lb_finish_blocks(lb, lb_status, lb_words, gridDim.x, &last_flag, mode == 2 || ir);
 }
 
 #ifdef HONU_STAGE_TIMING
@@ -571,7 +627,8 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
                                uint64_t data_cap, DecodeScratch *scratch, uint64_t *offs,
                                uint64_t *totals, LbState *lb, uint64_t *lb_status,
                                uint64_t *lb_gstatus, uint64_t lb_words, int max_blocks, uint32_t *spec_seen,
-                               uint32_t *recoveries, bool allow_spec, bool inplace, hipStream_t s) {
+                               uint32_t *recoveries, bool allow_spec, bool inplace, bool inline_rec,
+                               int guard_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
     // (32-record tiles for batches whose 64-record tiles fill at most half the
     // resident waves, so that every SIMD walks records, measured slower with
@@ -590,7 +647,7 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
     const dim3 grid((unsigned)b), block(HONU_BLOCK);
 #define HONU_FUSED_LAUNCH_F(M, F, I)                                                                      \
     hipLaunchKernelGGL((k_decode_fused<M, F, I>), grid, block, 0, s, rec, rec_off, n, O, lb, lb_status,    \
-                       lb_gstatus, lb_words, spec_seen, recoveries)
+                       lb_gstatus, lb_words, spec_seen, recoveries, inline_rec && !stat)
 #define HONU_FUSED_LAUNCH(M)                                                                               \
     do {                                                                                                   \
         if (stat && inplace) HONU_FUSED_LAUNCH_F(M, FORM_STATIC, true);                                     \
@@ -602,10 +659,26 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
         HONU_FUSED_LAUNCH(0);
         return hipGetLastError();
     }
-    // speculative launch, then the guarded recovery launch (a no-op unless a
-    // record failed after publishing its counts: malformed input only)
+    // speculative launch, then (static tiles, or inline recovery off) the
+    // guarded recovery launch (a no-op unless a record failed after publishing
+    // its counts or a speculated ACL list holds a nil entry)
     HONU_FUSED_LAUNCH(1);
-    HONU_FUSED_LAUNCH(2);
+    if (stat || !inline_rec) {
+        if (guard_blocks > 0 && (uint64_t)guard_blocks < b) {
+            // a guard of few workgroups (ticket tiles whatever the batch:
+            // deadlock-free with any grid) is placed sooner beside other
+            // kernels; a recovery then runs on those waves only
+            const dim3 g2((unsigned)guard_blocks);
+            if (inplace)
+                hipLaunchKernelGGL((k_decode_fused<2, FORM_TICKET, true>), g2, block, 0, s, rec, rec_off, n, O, lb,
+                                   lb_status, lb_gstatus, lb_words, spec_seen, recoveries, false);
+            else
+                hipLaunchKernelGGL((k_decode_fused<2, FORM_TICKET, false>), g2, block, 0, s, rec, rec_off, n, O, lb,
+                                   lb_status, lb_gstatus, lb_words, spec_seen, recoveries, false);
+        } else {
+            HONU_FUSED_LAUNCH(2);
+        }
+    }
 #undef HONU_FUSED_LAUNCH_F
 #undef HONU_FUSED_LAUNCH
     return hipGetLastError();

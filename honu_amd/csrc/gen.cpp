@@ -7,6 +7,7 @@
 // math/rand + crypto/rand) so that host and device, and every rank of a
 // multi-GPU run, see identical records for (seed, index).
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -46,7 +47,20 @@ const char kUserAgent[] = "Random User Agent v1";    // :300
 const uint64_t kOffSchema = 0, kLenSchema = 12;
 const uint64_t kOffMime = 12, kLenMime = 18;
 const uint64_t kOffUA = 30, kLenUA = 20;
-const uint64_t kVarHeader = 50;
+const uint64_t kVarHeader = 64;  // (the shared strings take 50 bytes; 16-aligned after them)
+
+// HONU_GEN_VAR_ALIGN=1: every frame body a record references (IP, public key
+// id, encryption key, HMAC secret, signature) starts 16-byte aligned in the
+// var arena, as a binding's flatten may lay them out, so the tail encoder's
+// aligned 16-byte frame loads do not straddle a block they do not need
+// (VERDICT r04 item 4). The encoded records are the same either way.
+bool var_align() {
+    static const int v = [] {
+        const char *e = getenv("HONU_GEN_VAR_ALIGN");
+        return e && *e ? atoi(e) : 0;
+    }();
+    return v != 0;
+}
 
 struct Rng {
     uint64_t s;
@@ -69,6 +83,7 @@ struct Sink {  // null pointers: counting only
 };
 
 void put_var(Sink &s, honu_span &sp, const uint8_t *src, uint64_t len) {
+    if (var_align()) s.var_n = (s.var_n + 15) & ~15ull;  // (part bases are 16-aligned, plan)
     sp.off = s.var_n;
     sp.len = len;
     if (s.var) memcpy(s.var + s.var_n, src, len);
@@ -254,7 +269,7 @@ std::vector<Part> plan(uint64_t seed, int shape, uint64_t first, uint64_t n) {
     parallel(nt, [&](int t) {
         Sink s{nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0};
         for (uint64_t i = 0; i < parts[t].n; i++) gen_one(seed, shape, parts[t].first + i, s, nullptr);
-        parts[t].var_n = s.var_n;
+        parts[t].var_n = var_align() ? (s.var_n + 15) & ~15ull : s.var_n;
         parts[t].acl_n = s.acl_n;
         parts[t].reg_n = s.reg_n;
         parts[t].pay_n = s.pay_n;

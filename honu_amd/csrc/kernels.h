@@ -149,7 +149,8 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
                                uint64_t data_cap, DecodeScratch *scratch, uint64_t *offs,
                                uint64_t *totals, LbState *lb, uint64_t *lb_status,
                                uint64_t *lb_gstatus, uint64_t lb_words, int max_blocks, uint32_t *spec_seen,
-                               uint32_t *recoveries, bool allow_spec, bool inplace, hipStream_t s);
+                               uint32_t *recoveries, bool allow_spec, bool inplace, bool inline_rec,
+                               int guard_blocks, hipStream_t s);
 
 hipError_t launch_decode_parse_win(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                    honu_meta *meta, honu_record_info *info,

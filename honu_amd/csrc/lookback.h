@@ -9,9 +9,11 @@
 // at once (one per lane), sums back to the nearest inclusive prefix and
 // spins only while a tile in between has not published.
 //
-// Status word: bits 63:62 flag (0 none, 1 aggregate, 2 inclusive), 61:44 the
-// launch epoch (18 bits), 43:0 the value (< 2^44: the counts are bounded by the
-// bytes of one arena). Words of earlier launches carry another epoch, so the
+// Status word: bits 63:62 flag (0 none, 1 aggregate, 2 inclusive), 61:43 the
+// tag: the launch epoch (18 bits) and, above it, the pass (the single-launch
+// decode's in-launch recovery pass writes pass-1 words over the pass-0 ones,
+// fused.hip), 42:0 the value (< 2^43: the counts are bounded by the bytes of
+// one arena). Words of earlier launches carry another epoch, so the
 // array is never cleared between launches; the end of a launch resets the
 // ticket, advances the epoch and, when the epoch wraps, clears the array:
 // lb_finish_blocks (the last workgroup to finish) ends every single-launch
@@ -32,14 +34,30 @@ struct LbState {
     uint32_t done;     // workgroups finished (static tiles, lb_finish_blocks)
     uint32_t epoch;
     uint32_t misspec;  // speculative decode: a tile published counts that changed (fused.hip)
+    uint32_t ticket2;  // next tile of the in-launch recovery pass (fused.hip)
+    uint32_t _pad0[27];
+    // in-launch recovery counters, polled by the waves that finished early: a
+    // line of their own, away from the ticket the other waves still take
+    uint32_t tdone;    // tiles of the speculative pass finished
+    uint32_t rdone;    // tiles whose stores were released before the recovery pass
+    uint32_t _pad1[30];
 };
+static_assert(sizeof(LbState) == 256, "two 128-byte lines");
 
 constexpr uint32_t LB_EPOCH_BITS = 18;
 constexpr uint32_t LB_EPOCH_MASK = (1u << LB_EPOCH_BITS) - 1;
-constexpr uint64_t LB_VAL_MASK = (1ull << 44) - 1;
+constexpr uint32_t LB_PASS_BIT = 1u << LB_EPOCH_BITS;  // in a tag: the recovery pass
+constexpr uint32_t LB_TAG_MASK = (1u << (LB_EPOCH_BITS + 1)) - 1;
+constexpr uint32_t LB_TAG_SHIFT = 43;
+constexpr uint64_t LB_VAL_MASK = (1ull << LB_TAG_SHIFT) - 1;
 
-HONU_DEV uint64_t lb_word(uint32_t flag, uint32_t epoch, uint64_t v) {
-    return ((uint64_t)flag << 62) | ((uint64_t)(epoch & LB_EPOCH_MASK) << 44) | (v & LB_VAL_MASK);
+// tag: the launch epoch, | LB_PASS_BIT in a recovery pass
+HONU_DEV uint64_t lb_word(uint32_t flag, uint32_t tag, uint64_t v) {
+    return ((uint64_t)flag << 62) | ((uint64_t)(tag & LB_TAG_MASK) << LB_TAG_SHIFT) | (v & LB_VAL_MASK);
+}
+// a word of this launch (and pass)?
+HONU_DEV bool lb_tagged(uint64_t w, uint32_t tag) {
+    return (w >> 62) != 0 && ((uint32_t)(w >> LB_TAG_SHIFT) & LB_TAG_MASK) == (tag & LB_TAG_MASK);
 }
 HONU_DEV uint64_t lb_load(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -55,20 +73,17 @@ HONU_DEV uint32_t lb_epoch(LbState *s) {
 
 // The ticket atomic alone (lane 0's return value; read it with
 // readlane(v, 0) when needed, so its round trip overlaps other work).
-HONU_DEV uint32_t lb_ticket_issue(LbState *s) {
+// ctr: &LbState::ticket, or ::ticket2 in a recovery pass.
+HONU_DEV uint32_t lb_ticket_issue(uint32_t *ctr) {
     uint32_t t = 0;
-    if (lane_id() == 0)
-        t = __hip_atomic_fetch_add(&s->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane_id() == 0) t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return t;
 }
+HONU_DEV uint32_t lb_ticket_issue(LbState *s) { return lb_ticket_issue(&s->ticket); }
 
 // Next tile for this wave (wave-uniform).
-HONU_DEV uint64_t lb_ticket(LbState *s) {
-    uint32_t t = 0;
-    if (lane_id() == 0)
-        t = __hip_atomic_fetch_add(&s->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return __builtin_amdgcn_readlane(t, 0);
-}
+HONU_DEV uint64_t lb_ticket(uint32_t *ctr) { return __builtin_amdgcn_readlane(lb_ticket_issue(ctr), 0); }
+HONU_DEV uint64_t lb_ticket(LbState *s) { return lb_ticket(&s->ticket); }
 
 // Tile t of the launch with per-column aggregates agg[c] (wave-uniform):
 // publishes them, returns the exclusive prefixes of the tile in excl[c] and
@@ -116,7 +131,7 @@ HONU_DEV void lb_resolve(uint64_t *status, uint64_t t, uint32_t ep, const uint64
             const uint64_t w = idx >= 0 ? lb_load(status + (uint64_t)idx * K + c)
                                         : lb_word(2, ep, 0);  // before tile 0: prefix 0
             const uint32_t fl = (uint32_t)(w >> 62);
-            const bool ready = fl != 0 && ((uint32_t)(w >> 44) & LB_EPOCH_MASK) == (ep & LB_EPOCH_MASK);
+            const bool ready = lb_tagged(w, ep);
             const uint64_t nb = __ballot(!ready);
             const uint64_t ib = __ballot(ready && fl == 2);
             const uint32_t p = ib ? (uint32_t)__builtin_ctzll(ib) : 64;  // nearest inclusive
@@ -177,7 +192,7 @@ HONU_DEV void lb_resolve_grouped(uint64_t *status, uint64_t *gstatus, uint64_t t
             const uint64_t *src = grp ? gstatus + (uint64_t)lane * K + col
                                       : status + (g * HONU_WAVE + lane) * K + col;
             const uint64_t w = lane < n_in ? lb_load(src) : lb_word(1, ep, 0);
-            const bool ready = (w >> 62) != 0 && ((uint32_t)(w >> 44) & LB_EPOCH_MASK) == (ep & LB_EPOCH_MASK);
+            const bool ready = lb_tagged(w, ep);
             if (__ballot(!ready)) continue;
             const uint64_t sum = wave_sum(w & LB_VAL_MASK);
             excl[col] += sum;
@@ -220,7 +235,7 @@ HONU_DEV void lb_resolve_grouped_lb(uint64_t *status, uint64_t *gstatus, uint64_
             if (!(todo & (1u << c))) continue;
             if (c < K) {
                 const uint64_t w = lane < r ? lb_load(status + (g * HONU_WAVE + lane) * K + c) : lb_word(1, ep, 0);
-                const bool ready = (w >> 62) != 0 && ((uint32_t)(w >> 44) & LB_EPOCH_MASK) == (ep & LB_EPOCH_MASK);
+                const bool ready = lb_tagged(w, ep);
                 if (__ballot(!ready)) continue;
                 in_sum[c] = wave_sum(w & LB_VAL_MASK);
                 excl[c] += in_sum[c];
@@ -231,7 +246,7 @@ HONU_DEV void lb_resolve_grouped_lb(uint64_t *status, uint64_t *gstatus, uint64_
                 const int64_t idx = top[col] - (int64_t)lane;  // lane 0: the nearest group
                 const uint64_t w = idx >= 0 ? lb_load(gstatus + (uint64_t)idx * K + col) : lb_word(2, ep, 0);
                 const uint32_t fl = (uint32_t)(w >> 62);
-                const bool ready = fl != 0 && ((uint32_t)(w >> 44) & LB_EPOCH_MASK) == (ep & LB_EPOCH_MASK);
+                const bool ready = lb_tagged(w, ep);
                 const uint64_t nb = __ballot(!ready), ib = __ballot(ready && fl == 2);
                 const uint32_t p = ib ? (uint32_t)__builtin_ctzll(ib) : 64;
                 const uint64_t upto = p >= 63 ? ~0ull : ((2ull << p) - 1);
@@ -248,6 +263,18 @@ HONU_DEV void lb_resolve_grouped_lb(uint64_t *status, uint64_t *gstatus, uint64_
 #pragma unroll
         for (int c = 0; c < K; c++)
             if (lane == (uint32_t)c) lb_store(gstatus + g * K + c, lb_word(2, ep, excl[c] + agg[c]));
+    }
+}
+
+// Spin (wave-uniform) until *ctr >= target: the in-launch recovery's waits
+// for the tiles of a pass, which running waves hold (fused.hip).
+HONU_DEV void lb_wait_count(uint32_t *ctr, uint64_t target) {
+    for (;;) {
+        uint32_t d = 0;
+        if (lane_id() == 0) d = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint64_t)__builtin_amdgcn_readlane(d, 0) >= target) return;
+        // ~0.9 us between polls: up to ~2,000 waiting waves poll one address
+        __builtin_amdgcn_s_sleep(32);
     }
 }
 
@@ -302,6 +329,9 @@ HONU_DEV void lb_finish_blocks(LbState *s, uint64_t *status, uint64_t status_wor
     if (threadIdx.x == 0) {
         __hip_atomic_store(&s->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&s->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&s->ticket2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&s->tdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&s->rdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (clear_misspec) __hip_atomic_store(&s->misspec, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&s->epoch, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }

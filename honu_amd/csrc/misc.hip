@@ -216,7 +216,8 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_verify_decoded(
 // each wave a contiguous range (the layout of the codec's copy engine) with 8
 // chunks per lane in flight, or grid-stride with 4 (the guide's float4 copy).
 // ------------------------------------------------------------------------
-template <int MODE>  // 0 read, 1 write, 2 copy (wave ranges), 3 copy (grid stride)
+template <int MODE>  // 0 read, 1 write, 2 copy (wave ranges), 3 copy (grid stride), 4 copy
+                     // (wave ranges, non-temporal loads and stores)
 __global__ __launch_bounds__(HONU_BLOCK) void k_hbm_probe(const u32x4 *__restrict__ a, u32x4 *__restrict__ b,
                                                           uint64_t n, uint32_t *__restrict__ sink) {
     const uint32_t lane = lane_id();
@@ -244,13 +245,15 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_hbm_probe(const u32x4 *__restric
         if constexpr (MODE != 1) {
 #pragma unroll
             for (int u = 0; u < U; u++)
-                if (i + u * HONU_WAVE < hi) v[u] = a[i + u * HONU_WAVE];
+                if (i + u * HONU_WAVE < hi)
+                    v[u] = MODE == 4 ? __builtin_nontemporal_load(a + i + u * HONU_WAVE) : a[i + u * HONU_WAVE];
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (i + u * HONU_WAVE >= hi) continue;
             if constexpr (MODE == 0) acc ^= v[u];
             else if constexpr (MODE == 1) b[i + u * HONU_WAVE] = u32x4{(uint32_t)i, (uint32_t)u, 1, 2};
+            else if constexpr (MODE == 4) __builtin_nontemporal_store(v[u], b + i + u * HONU_WAVE);
             else b[i + u * HONU_WAVE] = v[u];
         }
     }
@@ -267,7 +270,8 @@ hipError_t launch_hbm_probe(int mode, const void *src, void *dst, uint64_t bytes
     case 0: hipLaunchKernelGGL(k_hbm_probe<0>, dim3(blocks), dim3(HONU_BLOCK), 0, s, a, b, n, sink); break;
     case 1: hipLaunchKernelGGL(k_hbm_probe<1>, dim3(blocks), dim3(HONU_BLOCK), 0, s, a, b, n, sink); break;
     case 2: hipLaunchKernelGGL(k_hbm_probe<2>, dim3(blocks), dim3(HONU_BLOCK), 0, s, a, b, n, sink); break;
-    default: hipLaunchKernelGGL(k_hbm_probe<3>, dim3(blocks), dim3(HONU_BLOCK), 0, s, a, b, n, sink); break;
+    case 3: hipLaunchKernelGGL(k_hbm_probe<3>, dim3(blocks), dim3(HONU_BLOCK), 0, s, a, b, n, sink); break;
+    default: hipLaunchKernelGGL(k_hbm_probe<4>, dim3(blocks), dim3(HONU_BLOCK), 0, s, a, b, n, sink); break;
     }
     return hipGetLastError();
 }

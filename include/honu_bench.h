@@ -89,7 +89,9 @@ uint64_t honu_digest_host(const uint8_t *p, uint64_t len);
  * roofline denominator beside the 8 TB/s spec). mode 0 reads bytes of d_src,
  * 1 writes bytes of d_dst, 2 copies d_src -> d_dst with each wave on a
  * contiguous range (the codec copy engine's layout, 8 x 16 B per lane in
- * flight), 3 the same copy grid-stride (4 x 16 B per lane). bytes is rounded
+ * flight), 3 the same copy grid-stride (4 x 16 B per lane), 4 mode 2 with
+ * non-temporal loads and stores (tools/copy_sweep.hip: the fastest plain copy
+ * form measured on this part, at 4 workgroups per CU). bytes is rounded
  * down to 16; buffers 16-byte aligned; blocks_per_cu 0 = 2. Asynchronous on
  * stream; time it with events. */
 int32_t honu_hbm_probe(honu_ctx *ctx, int32_t mode, const void *d_src, void *d_dst, uint64_t bytes,

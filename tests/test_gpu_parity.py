@@ -637,13 +637,13 @@ def test_encode_writer_drain_bounds(codec, oracle_lib):
 
 
 def test_hbm_probe_modes(codec):
-    """honu_hbm_probe (bench.py's achievable-rate denominator): both copy forms
-    move every byte (sizes not a multiple of a wave's chunk), the write form
-    fills the buffer, bad arguments are refused."""
+    """honu_hbm_probe (bench.py's achievable-rate denominator): the three copy
+    forms move every byte (sizes not a multiple of a wave's chunk), the write
+    form fills the buffer, bad arguments are refused."""
     L = hobj._lib
     for nbytes in (16, 4096 + 48, (3 << 20) + 16 * 77):
         a = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device=codec.torch_device)
-        for mode in (2, 3):
+        for mode in (2, 3, 4):
             for bpc in (0, 1, 4):
                 b = torch.zeros_like(a)
                 L.check(codec.lib.honu_hbm_probe(codec.ctx, mode, L.ptr(a), L.ptr(b), nbytes, bpc,

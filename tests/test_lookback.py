@@ -205,17 +205,23 @@ def test_speculative_publish_recovers(oracle_lib, n, bad, inplace):
         c.close()
 
 
+@pytest.mark.parametrize("inline_rec,guard_blocks", [(1, 0), (0, 0), (0, 16)],
+                         ids=["in_launch", "guard_launch", "small_guard"])
 @FORMS
-@pytest.mark.parametrize("n,k", [(140000, 1), (140000, 200)])
-def test_speculative_acl_flags_recover(oracle_lib, n, k, inplace):
+@pytest.mark.parametrize("n,k", [(140000, 1), (140000, 200), (100000, 1), (100000, 200)])
+def test_speculative_acl_flags_recover(oracle_lib, n, k, inplace, inline_rec, guard_blocks):
     """Speculative launches also take every ACL list that fits its record as
     all present without gathering its entry flags in the walk; the table fill
     (table form) or the flag gather after the publish (in-place form, fused.hip
     flag_gather / flag_check) checks them. Records whose lists hold nil entries (the walk
     then read every later field at the wrong place) are spliced into a
-    2188-tile batch: the fill must raise misspec and the guarded launch redo
-    the batch bit-exact with the oracle; a clean batch decoded next on the same
-    context is exact too."""
+    2188-tile batch (ticket tiles) or a 1563-tile one (static tiles): the check
+    must raise misspec and the batch be decoded again, bit-exact with the
+    oracle, by the guarded second launch (inline_recovery 0, the default), by
+    a guarded launch of 16 workgroups (guard_blocks 16: ticket tiles over
+    64 waves, also after a static speculative launch), or by the launch's own
+    recovery pass (inline_recovery 1; static tiles keep the guard); a clean
+    batch decoded next on the same context is exact too."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from corpora import random_metas
@@ -242,6 +248,8 @@ def test_speculative_acl_flags_recover(oracle_lib, n, k, inplace):
     c = hobj.Codec(0, n)
     try:
         hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
+        hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"inline_recovery", inline_rec), "param")
+        hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"guard_blocks", guard_blocks), "param")
         r0 = _get(c, b"recoveries")
         d = _Dec(c, brec, boff, inplace)
         assert d() == 0

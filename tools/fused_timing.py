@@ -40,11 +40,14 @@ def main():
     ap.add_argument("--shape", default="small")
     ap.add_argument("--records", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--acl-inplace", type=int, default=1, choices=[0, 1],
+                    help="context param acl_inplace: 1 the in-place ACL lists (default), 0 the table")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     n = a.records
     codec = Codec(0, n)
     L, c = codec.lib, codec.ctx
+    _lib.check(L.honu_ctx_set_param(c, b"acl_inplace", a.acl_inplace), "param")
     meta, var, acl, reg, off = gen_meta(1, a.shape, 0, n)
 
     def D(x):
@@ -98,7 +101,7 @@ def main():
     assert fn(buf.ctypes.data, waves, 0) == 0
     ntiles = (n + 63) // 64
     per_tile = buf.astype(np.float64).sum(axis=0) / ntiles / 100.0  # us
-    res = {"shape": a.shape, "records": n, "tiles": ntiles, "waves": waves,
+    res = {"shape": a.shape, "records": n, "acl_inplace": a.acl_inplace, "tiles": ntiles, "waves": waves,
            "kernel_ms_unstamped": min(ms),
            "stage_us_per_tile": {k: round(float(per_tile[i]), 3) for i, k in enumerate(STAGES)},
            "tile_us_total": round(float(per_tile[: len(STAGES)].sum()), 3),
