@@ -116,6 +116,13 @@ def parse_args(argv=None):
                    help="1: a chunk's single-launch decode (and its guarded launch) on a high-priority "
                         "stream of its slot, so the guard's workgroups are dispatched before the other "
                         "slot's metadata kernels when CUs free up")
+    p.add_argument("--slots", type=int, default=2,
+                   help="output slots (chunks in flight); 3 lets a chunk's encode run while the two "
+                        "before it are still being decoded (with --copy-order ahead)")
+    p.add_argument("--copy-order", choices=["chunk", "ahead"], default="chunk",
+                   help="chunk: a chunk's decode copy right after its encode copy on the copy stream; "
+                        "ahead: after the NEXT chunk's encode copy, so the copy stream does not wait "
+                        "for a chunk's Metadata decode")
     p.add_argument("--decode-chain", type=int, default=1, choices=[0, 1],
                    help="with two metadata streams, a chunk's single-launch decode waits for the "
                         "previous chunk's (and its guarded launch): the guard never queues for "
@@ -219,7 +226,7 @@ class Bench:
         self.ncu = torch.cuda.get_device_properties(self.dev).multi_processor_count
         if not pipeline:
             return
-        nslots = 1 if args.serial else 2
+        nslots = 1 if args.serial else max(2, getattr(args, "slots", 2))
         self.slots = [Slot(self.dev, C, self.out_cap, self.acl_cap, self.reg_cap,
                            16 if encode_only else self.data_cap) for _ in range(nslots)]
         ncu = torch.cuda.get_device_properties(self.dev).multi_processor_count
@@ -250,19 +257,19 @@ class Bench:
         self.sm = torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio < 0 else 0)  # metadata kernels
         # payload copies: the bandwidth-bound critical path, dispatched first
         self.sc = (torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio > 0 else 0)
-                   if nslots == 2 else self.sm)
-        if args.meta_cu_stride and nslots == 2:  # metadata and copies on their own CUs
+                   if nslots >= 2 else self.sm)
+        if args.meta_cu_stride and nslots >= 2:  # metadata and copies on their own CUs
             S = args.meta_cu_stride
             self.sm = cu_masked_stream(self.dev, ncu, lambda i: i % S == 0)
             if args.copy_cu_mask == "rest":
                 self.sc = cu_masked_stream(self.dev, ncu, lambda i: i % S != 0)
         # --meta-streams 2: slot k's metadata kernels on stream k (its own context)
         self.sms = [self.sm]
-        if getattr(args, "meta_streams", 1) == 2 and nslots == 2 and not args.meta_cu_stride:
+        if getattr(args, "meta_streams", 1) == 2 and nslots >= 2 and not args.meta_cu_stride:
             self.sms.append(torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio < 0 else 0))
         # --copy-streams 2: decode copies on their own stream
         self.sd = self.sc
-        if getattr(args, "copy_streams", 1) == 2 and nslots == 2 and not args.meta_cu_stride:
+        if getattr(args, "copy_streams", 1) == 2 and nslots >= 2 and not args.meta_cu_stride:
             self.sd = torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio > 0 else 0)
         # --decode-prio: one high-priority decode stream per metadata stream
         self.sdec = [torch.cuda.Stream(self.dev, priority=-1) for _ in self.sms] \
@@ -273,6 +280,10 @@ class Bench:
         self.nchunk = 0  # chunks issued so far, across steps: slots alternate globally
         self.enc_done = None  # the last issued chunk's encode copy (--meta-beside decode)
         self.dec_done = None  # the last issued chunk's single-launch decode (--decode-chain)
+        # --copy-order ahead: the last chunk's decode copy, issued after the
+        # next chunk's encode copy (flush() issues it)
+        self.ahead = getattr(args, "copy_order", "chunk") == "ahead" and nslots >= 2 and not encode_only
+        self.pending_dec = None
         torch.cuda.synchronize()
 
     def _sizes(self, codec, a, b, out_off, status, s):
@@ -307,6 +318,8 @@ class Bench:
                 if pending is not None:
                     ok &= self._check(check, pending)
                 pending = (a, b, sl)
+        if check is not None:
+            self.flush()
         if pending is not None:
             ok &= self._check(check, pending)
         torch.cuda.current_stream(self.dev).wait_stream(self.sc)
@@ -314,6 +327,13 @@ class Bench:
         for sm in self.sms + (self.sdec or []):
             torch.cuda.current_stream(self.dev).wait_stream(sm)
         return ok
+
+    def flush(self):
+        """--copy-order ahead: issue the decode copy still held back (the
+        timed region issues its last one before it ends)."""
+        dec, self.pending_dec = self.pending_dec, None
+        if dec is not None:
+            dec()
 
     def _check(self, check, pending):
         a, b, sl = pending
@@ -402,21 +422,30 @@ class Bench:
             e1.record(sc)
         self.enc_done = torch.cuda.Event()
         self.enc_done.record(sc)
-        sd = self.sd  # the decode copy: after this chunk's encode copy and its table fill
-        if sd is not sc:
-            sd.wait_event(self.enc_done)
-        sd.wait_event(ev_fill)
-        e2 = torch.cuda.Event(enable_timing=True) if timed else None
-        e3 = torch.cuda.Event(enable_timing=True) if timed else None
-        if timed:
-            e2.record(sd)
-        _lib.check(L.honu_decode_payloads(c, P(sl.out), n, P(sl.dinfo), P(sl.data),
-                                          P(sl.totals), sd.cuda_stream), "decode_payloads")
-        if timed:
-            e3.record(sd)
-            self.events.append((a, b, e0, e1, e2, e3))
-        sl.free = torch.cuda.Event()
-        sl.free.record(sd)
+        enc_done = self.enc_done
+
+        def dec():  # the decode copy: after this chunk's encode copy and its table fill
+            sd = self.sd
+            if sd is not sc:
+                sd.wait_event(enc_done)
+            sd.wait_event(ev_fill)
+            e2 = torch.cuda.Event(enable_timing=True) if timed else None
+            e3 = torch.cuda.Event(enable_timing=True) if timed else None
+            if timed:
+                e2.record(sd)
+            _lib.check(L.honu_decode_payloads(c, P(sl.out), n, P(sl.dinfo), P(sl.data),
+                                              P(sl.totals), sd.cuda_stream), "decode_payloads")
+            if timed:
+                e3.record(sd)
+                self.events.append((a, b, e0, e1, e2, e3))
+            sl.free = torch.cuda.Event()
+            sl.free.record(sd)
+        if self.ahead:  # the previous chunk's decode copy after this chunk's encode copy
+            prev, self.pending_dec = self.pending_dec, dec
+            if prev is not None:
+                prev()
+        else:
+            dec()
         self.last = (a, b, sl)
         return sl
 
@@ -1385,6 +1414,7 @@ def pipeline_leg(args, shape, encode_only, rank, local, world, dist, barrier, ga
     bench = Bench(la, rank, local, encode_only=encode_only)
     for _ in range(la.warmup):
         bench.step()
+    bench.flush()
     torch.cuda.synchronize()
     rec0 = bench.recoveries()
     bench.events = []
@@ -1393,6 +1423,7 @@ def pipeline_leg(args, shape, encode_only, rank, local, world, dist, barrier, ga
     t0 = time.perf_counter()
     for _ in range(la.steps):
         bench.step(timed=True)
+    bench.flush()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -1532,6 +1563,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
     bench = Bench(args, rank, local)
     for _ in range(args.warmup):
         bench.step()
+    bench.flush()
     torch.cuda.synchronize()
     rec0 = bench.recoveries()  # count the timed steps' only
     bench.events = []
@@ -1540,6 +1572,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         bench.step(timed=True)
+    bench.flush()  # (--copy-order ahead: the last decode copy)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0

@@ -86,6 +86,46 @@ def test_bench_pipeline_bit_exact(oracle_lib, shape, n, after, decode, beside, m
     assert all(p != q for p, q in zip(slots, slots[1:]))
 
 
+@pytest.mark.parametrize("slots", [2, 3])
+@pytest.mark.parametrize("shape,n", [("small", 4000), ("mixed", 1200)])
+def test_bench_copy_order_ahead(oracle_lib, shape, n, slots):
+    """--copy-order ahead: chunk k's decode copy is issued after chunk k+1's
+    encode copy (and the last one by flush()); every chunk still decodes to
+    the oracle's bytes, with 2 and 3 slots in rotation."""
+    seed = 11
+    args = bench.parse_args(["--records", str(n), "--shape", shape, "--min-chunks", "5",
+                             "--seed", str(seed), "--copy-order", "ahead", "--slots", str(slots)])
+    b = bench.Bench(args, 0, 0)
+    assert b.ahead and len(b.slots) == slots
+    hb = gen_host_batch(seed, shape, 0, n)
+    seen = []
+
+    def check(a, z, sl):
+        sub = HostBatch(hb.meta[a:z], hb.var, hb.acl, hb.regions, hb.payload,
+                        hb.payload_off[a:z + 1])
+        oout, ooff, _ = oracle_lib.marshal_batch(sub)
+        assert _host(sl.out, int(ooff[-1])).tobytes() == oout.tobytes(), (a, z)
+        _, oinfo, _, _, odata, otot = oracle_lib.decode_batch(oout, ooff, True)
+        data = _host(sl.data, int(otot[2]))
+        for i in range(z - a):
+            o, ln = int(oinfo[i]["data_off"]), int(oinfo[i]["data_len"])
+            assert data[o:o + ln].tobytes() == odata[o:o + ln].tobytes(), (a + i)
+        assert b._verify_chunk(a, z, sl)
+        seen.append((a, z))
+        return True
+
+    for _ in range(2):  # the timed form (decode copies one chunk behind), then a checked step
+        b.step()
+    assert b.pending_dec is not None
+    b.flush()
+    assert b.pending_dec is None
+    for _ in range(2):
+        assert b.step(check=check)
+    torch.cuda.synchronize()
+    assert seen == b.chunks * 2
+    assert b.verify()
+
+
 def test_bench_verify_detects_corruption():
     """_verify_chunk (honu_verify_decoded + digests) flags one wrong byte in a
     decoded ObjectID, span, ACL entry (in place in the records arena: its
