@@ -46,7 +46,8 @@ struct honu_ctx {
     int enc_fork;            // honu_ctx_set_param("encode_fork", 0 off / 1 on / 2 auto: when lane_blocks caps the grid)
     bool acl_inplace;        // honu_ctx_set_param("acl_inplace"): decode returns all-present ACL lists in place
     bool inline_recovery;    // honu_ctx_set_param("inline_recovery"): ticket-form launches recover in-launch
-    int guard_blocks;        // honu_ctx_set_param("guard_blocks"): workgroups of the guarded launch (0: full grid)
+    int guard_blocks;        // honu_ctx_set_param("guard_blocks"): one-wave workgroups of the guarded launch
+                             // (0: as many as the speculative launch has waves)
 };
 static constexpr uint32_t SPEC_BACKOFF_CALLS = 16;
 

@@ -328,8 +328,14 @@ struct SpecPub {
 // tiles keep the guarded launch: their waves may wait on workgroups that are
 // not resident yet, so a launch-wide wait could deadlock beside another
 // persistent kernel.
-template <int MODE, int FORM, bool INPL>
-__global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
+//
+// WPB: waves per workgroup. The guarded launch runs one-wave workgroups
+// (19 KB of LDS each instead of 78 KB), so a no-op guard is placed beside the
+// other slot's tail encoder, whose two 64 KB workgroups per CU leave 32 KB
+// free (with 4-wave workgroups it waited 40-60 us there
+// in every Small step, profiles/r05/guard).
+template <int MODE, int FORM, bool INPL, int WPB = HONU_WAVES_PER_BLOCK>
+__global__ __launch_bounds__(WPB * HONU_WAVE, 2) void k_decode_fused(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
     DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t *lb_gstatus, uint64_t lb_words,
     uint32_t *spec_seen, uint32_t *recoveries, bool inline_rec) {
@@ -345,7 +351,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     }
     constexpr bool STAT = FORM != FORM_TICKET;
     constexpr uint32_t WAVE_BYTES = form_wave_bytes<FORM>();
-    __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * WAVE_BYTES];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[WPB * WAVE_BYTES];
     __shared__ uint32_t last_flag;
     __shared__ uint32_t wg_ticket;
     uint8_t *ws = smem + (threadIdx.x / HONU_WAVE) * WAVE_BYTES;
@@ -353,14 +359,14 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     const uint32_t ep = lb_epoch(lb);
     const uint64_t ntiles = (n + HONU_WAVE - 1) / HONU_WAVE;
     const bool ir = MODE == 1 && FORM == FORM_TICKET && inline_rec;  // in-launch recovery
-    const uint64_t waves = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
+    const uint64_t waves = (uint64_t)gridDim.x * WPB;
     // every tile has a resident wave of its own: static tiles (lookback.h)
     // (measured: taking the next ticket and loading its bounds before the
     // look-back wait, to overlap them with it, doubled the wait: tiles are
     // then handed out ~40 us before their waves start them, which spreads the
     // publish times of consecutive tiles)
     constexpr bool stat_idx = STAT;
-    uint64_t k_static = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + threadIdx.x / HONU_WAVE;
+    uint64_t k_static = (uint64_t)blockIdx.x * WPB + threadIdx.x / HONU_WAVE;
     WSTAMP_START();
     // ticket mode: the next tile's ticket is requested once the current tile's
     // last ACL staging round has landed (its table stores and the rest of the
@@ -373,7 +379,7 @@ __global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(
     bool tk_pending = false;
     if constexpr (!stat_idx) {  // the same in every wave of the workgroup
         if (threadIdx.x == 0)
-            wg_ticket = __hip_atomic_fetch_add(&lb->ticket, (uint32_t)HONU_WAVES_PER_BLOCK, __ATOMIC_RELAXED,
+            wg_ticket = __hip_atomic_fetch_add(&lb->ticket, (uint32_t)WPB, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
         tk = wg_ticket + threadIdx.x / HONU_WAVE;
@@ -664,20 +670,25 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
     // its counts or a speculated ACL list holds a nil entry)
     HONU_FUSED_LAUNCH(1);
     if (stat || !inline_rec) {
-        if (guard_blocks > 0 && (uint64_t)guard_blocks < b) {
-            // a guard of few workgroups (ticket tiles whatever the batch:
-            // deadlock-free with any grid) is placed sooner beside other
-            // kernels; a recovery then runs on those waves only
-            const dim3 g2((unsigned)guard_blocks);
-            if (inplace)
-                hipLaunchKernelGGL((k_decode_fused<2, FORM_TICKET, true>), g2, block, 0, s, rec, rec_off, n, O, lb,
-                                   lb_status, lb_gstatus, lb_words, spec_seen, recoveries, false);
-            else
-                hipLaunchKernelGGL((k_decode_fused<2, FORM_TICKET, false>), g2, block, 0, s, rec, rec_off, n, O, lb,
-                                   lb_status, lb_gstatus, lb_words, spec_seen, recoveries, false);
-        } else {
+        // one-wave workgroups, as many waves as the speculative launch had
+        // (guard_blocks > 0: that many), ticket tiles whatever the batch
+        // (deadlock-free with any grid, static or not)
+        uint64_t gw = b * HONU_WAVES_PER_BLOCK;
+        if (guard_blocks > 0 && (uint64_t)guard_blocks < gw) gw = (uint64_t)guard_blocks;
+        const dim3 g2((unsigned)gw), b2(HONU_WAVE);
+#ifdef HONU_AB  // (A/B build: HONU_GUARD_WIDE=1, the round-4 guard of four-wave workgroups)
+        static const bool wide = getenv("HONU_GUARD_WIDE") && atoi(getenv("HONU_GUARD_WIDE")) == 1;
+        if (wide) {
             HONU_FUSED_LAUNCH(2);
+            return hipGetLastError();
         }
+#endif
+        if (inplace)
+            hipLaunchKernelGGL((k_decode_fused<2, FORM_TICKET, true, 1>), g2, b2, 0, s, rec, rec_off, n, O, lb,
+                               lb_status, lb_gstatus, lb_words, spec_seen, recoveries, false);
+        else
+            hipLaunchKernelGGL((k_decode_fused<2, FORM_TICKET, false, 1>), g2, b2, 0, s, rec, rec_off, n, O, lb,
+                               lb_status, lb_gstatus, lb_words, spec_seen, recoveries, false);
     }
 #undef HONU_FUSED_LAUNCH_F
 #undef HONU_FUSED_LAUNCH
