@@ -329,13 +329,9 @@ struct SpecPub {
 // not resident yet, so a launch-wide wait could deadlock beside another
 // persistent kernel.
 //
-// WPB: waves per workgroup. The guarded launch runs one-wave workgroups
-// (19 KB of LDS each instead of 78 KB), so a no-op guard is placed beside the
-// other slot's tail encoder, whose two 64 KB workgroups per CU leave 32 KB
-// free (with 4-wave workgroups it waited 40-60 us there
-// in every Small step, profiles/r05/guard).
-template <int MODE, int FORM, bool INPL, int WPB = HONU_WAVES_PER_BLOCK>
-__global__ __launch_bounds__(WPB * HONU_WAVE, 2) void k_decode_fused(
+// WPB: waves per workgroup (4; the guarded launch, k_decode_guard below: 1).
+template <int MODE, int FORM, bool INPL, int WPB>
+HONU_DEV void decode_fused_body(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
     DecodeOut O, LbState *lb, uint64_t *lb_status, uint64_t *lb_gstatus, uint64_t lb_words,
     uint32_t *spec_seen, uint32_t *recoveries, bool inline_rec) {
@@ -613,6 +609,31 @@ __global__ __launch_bounds__(WPB * HONU_WAVE, 2) void k_decode_fused(
     lb_finish_blocks(lb, lb_status, lb_words, gridDim.x, &last_flag, mode == 2 || ir);
 }
 
+#define HONU_FUSED_PARAMS                                                                             \
+    const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n, DecodeOut O,   \
+        LbState *lb, uint64_t *lb_status, uint64_t *lb_gstatus, uint64_t lb_words, uint32_t *spec_seen, \
+        uint32_t *recoveries, bool inline_rec
+#define HONU_FUSED_ARGS rec, rec_off, n, O, lb, lb_status, lb_gstatus, lb_words, spec_seen, recoveries, inline_rec
+
+template <int MODE, int FORM, bool INPL>
+__global__ __launch_bounds__(HONU_BLOCK, 2) void k_decode_fused(HONU_FUSED_PARAMS) {
+    decode_fused_body<MODE, FORM, INPL, HONU_WAVES_PER_BLOCK>(HONU_FUSED_ARGS);
+}
+
+// The guarded launch (MODE 2, ticket tiles) in one-wave workgroups of 19 KB
+// LDS (the four-wave ones take 78 KB). Where a no-op guard still waits is
+// registers, not LDS: beside the other slot's tail encoder (k_encode_meta_lane,
+// 180 VGPRs at 2 waves per SIMD: 144 of a SIMD's 512 free) no decode wave fits
+// (227-255 VGPRs; capped by amdgpu_num_vgpr the walk still needs 169 with 105
+// spilled), so it waits 25-60 us for an encoder wave to end in every Small
+// step; beside the copies and the other kernels it takes 4-6 us (1M Mixed:
+// every guard, profiles/r05/guard). VERDICT r04 item 5.
+template <bool INPL>
+__global__ __launch_bounds__(HONU_WAVE) void k_decode_guard(
+    HONU_FUSED_PARAMS) {
+    decode_fused_body<2, FORM_TICKET, INPL, 1>(HONU_FUSED_ARGS);
+}
+
 #ifdef HONU_STAGE_TIMING
 extern "C" int32_t honu_debug_stage_times(void *host, uint64_t waves, int32_t reset) {
     if (reset) {
@@ -684,11 +705,11 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
         }
 #endif
         if (inplace)
-            hipLaunchKernelGGL((k_decode_fused<2, FORM_TICKET, true, 1>), g2, b2, 0, s, rec, rec_off, n, O, lb,
-                               lb_status, lb_gstatus, lb_words, spec_seen, recoveries, false);
+            hipLaunchKernelGGL((k_decode_guard<true>), g2, b2, 0, s, rec, rec_off, n, O, lb, lb_status,
+                               lb_gstatus, lb_words, spec_seen, recoveries, false);
         else
-            hipLaunchKernelGGL((k_decode_fused<2, FORM_TICKET, false, 1>), g2, b2, 0, s, rec, rec_off, n, O, lb,
-                               lb_status, lb_gstatus, lb_words, spec_seen, recoveries, false);
+            hipLaunchKernelGGL((k_decode_guard<false>), g2, b2, 0, s, rec, rec_off, n, O, lb, lb_status,
+                               lb_gstatus, lb_words, spec_seen, recoveries, false);
     }
 #undef HONU_FUSED_LAUNCH_F
 #undef HONU_FUSED_LAUNCH

@@ -218,8 +218,8 @@ def test_speculative_acl_flags_recover(oracle_lib, n, k, inplace, inline_rec, gu
     2188-tile batch (ticket tiles) or a 1563-tile one (static tiles): the check
     must raise misspec and the batch be decoded again, bit-exact with the
     oracle, by the guarded second launch (inline_recovery 0, the default), by
-    a guarded launch of 16 workgroups (guard_blocks 16: ticket tiles over
-    64 waves, also after a static speculative launch), or by the launch's own
+    a guarded launch of 16 one-wave workgroups (guard_blocks 16: ticket
+    tiles over 16 waves, also after a static speculative launch), or by the launch's own
     recovery pass (inline_recovery 1; static tiles keep the guard); a clean
     batch decoded next on the same context is exact too."""
     if not torch.cuda.is_available():

@@ -26,7 +26,7 @@ def main():
         rows = sorted(csv.DictReader(f), key=lambda r: int(r["Start_Timestamp"]))
     dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6  # noqa: E731
     out = {"bench": bench}
-    g = [r for r in rows if "k_decode_fused<2" in r["Kernel_Name"]]
+    g = [r for r in rows if "k_decode_fused<2" in r["Kernel_Name"] or "k_decode_guard" in r["Kernel_Name"]]
     if g:
         out["guarded_launches"] = {"count": len(g),
                                    "avg_us": sum(dur(r) for r in g) / len(g) * 1e3}

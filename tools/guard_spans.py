@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Spans of the single-launch decode's launches in a rocprofv3 kernel trace
 (a guarded launch that queues for CUs): for every
-k_decode_fused<MODE,...> instantiation the count, median, mean and max
-duration, and for guarded launches (MODE 2) longer than --slow-us the
+k_decode_fused<MODE,...> / k_decode_guard<...> instantiation the count,
+median, mean and max duration, and for guarded launches (MODE 2: the
+k_decode_guard kernel since round 5) longer than --slow-us the
 kernels that ran beside them.
 
   python tools/guard_spans.py <run_results.db | *_kernel_trace.csv> [--slow-us 20]
@@ -40,7 +41,7 @@ def main():
     rows = load(a.trace)
     spans = collections.defaultdict(list)
     for n, s, e in rows:
-        if "k_decode_fused<" in n:
+        if "k_decode_fused<" in n or "k_decode_guard<" in n:
             spans[short(n)].append((e - s) / 1e3)
     out = {"trace": a.trace, "launches": {}}
     for k, v in sorted(spans.items()):
@@ -48,7 +49,7 @@ def main():
                               "mean_us": round(sum(v) / len(v), 1), "max_us": round(max(v), 1)}
     slow = []
     for n, s, e in rows:
-        if "k_decode_fused<2" in n and (e - s) / 1e3 > a.slow_us:
+        if ("k_decode_fused<2" in n or "k_decode_guard<" in n) and (e - s) / 1e3 > a.slow_us:
             beside = sorted({short(n2) for n2, s2, e2 in rows if s2 < e and e2 > s and (n2, s2) != (n, s)})
             slow.append({"us": round((e - s) / 1e3, 1), "beside": beside})
     out["guards_over_slow_us"] = len(slow)
