@@ -461,6 +461,18 @@ HONU_DEV void decode_fused_body(
         const bool igather = INPL && early.spec_acl && __ballot(ichk);  // wave-uniform
         if (igather) flag_gather(ws, rec, ichk ? (P.acl_pos & GRP_POS_MASK) : 0, ichk ? P.nacl : 0, 0);
         WSTAMP(10);  // publish + rows out + first staging round issued
+#if defined(HONU_STAGE_TIMING) && defined(HONU_STAGE_DRAIN)
+        // (timing variant: the wave's outstanding stores and loads drained
+        // first, stamped as stage 14, so stage 11 is the look-back alone.
+        // Measured: the drain is 0.08 us of a tile, the wait is the look-back
+        // itself, 9.6 us on 1M Small, 7.3 us on a 62 K Large chunk; the
+        // look-back's first loads issued before the row stores changed
+        // nothing: profiles/r05/lookback/)
+        if (INPL) {
+            __builtin_amdgcn_s_waitcnt(0);
+            WSTAMP(14);
+        }
+#endif
         if constexpr (STAT)  // every tile runs at once: grouped prefixes (lookback.h)
             lb_resolve_grouped<3>(lb_status, lb_gstatus, t, ntiles, tag, agg, excl);
         else  // tickets: a decoupled look-back over the group totals (the plain
