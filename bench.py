@@ -787,8 +787,11 @@ class DecodeBench:
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": gbs / HBM_PEAK_GBS,
-                "traffic": (pmc_traffic(self.workload("zero_copy"), "k_decode_fused<1")
-                            or pmc_traffic(self.workload("zero_copy"), "k_decode_fused<0")),
+                # the in-place form's kernels (the PMC run also holds the
+                # table form's, <..., false>, measured first)
+                "traffic": (pmc_traffic(self.workload("zero_copy"), "k_decode_fused<1, 0, true>")
+                            or pmc_traffic(self.workload("zero_copy"), "k_decode_fused<1, 1, true>")
+                            or pmc_traffic(self.workload("zero_copy"), "k_decode_fused<0, 0, true>")),
                 "avg_launch_ms": t * 1e3,
                 "algorithmic_bytes_per_launch": self.meta_bytes,
                 "algorithmic_bytes": "8 (offsets) + header + Metadata tail read; 352 row + 32 info "

@@ -46,7 +46,6 @@ struct honu_ctx {
     int enc_fork;            // honu_ctx_set_param("encode_fork", 0 off / 1 on / 2 auto: when lane_blocks caps the grid)
     bool acl_inplace;        // honu_ctx_set_param("acl_inplace"): decode returns all-present ACL lists in place
     bool inline_recovery;    // honu_ctx_set_param("inline_recovery"): ticket-form launches recover in-launch
-    uint64_t copy_base[3];   // the ticket copies' counters at their next launch (LaunchGeom::copy_base)
     int guard_blocks;        // honu_ctx_set_param("guard_blocks"): one-wave workgroups of the guarded launch
                              // (0: as many as the speculative launch has waves)
 };
@@ -210,8 +209,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     // lb_resolve_grouped*)
     const uint64_t groups = (tiles / HONU_WAVE + 1) > LB_GROUPS ? tiles / HONU_WAVE + 1 : LB_GROUPS;
     const uint64_t lb_dec_words = 3 * tiles + 3 * groups;
-    // + the copies' segment tickets (LaunchGeom::copy_ctr, 3 counters), cleared with it
-    const uint64_t lb_bytes = 2 * sizeof(LbState) + 8 * (lb_dec_words + scan_words) + 64;
+    const uint64_t lb_bytes = 2 * sizeof(LbState) + 8 * (lb_dec_words + scan_words);
     const uint64_t bytes = 8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 32 * n +
                            8 * n + 4 * map_cap + lb_bytes + 256;
     if (hipMalloc(&c->ws, bytes) != hipSuccess) {
@@ -263,8 +261,6 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->scan.words = scan_words;
     c->scan.max_blocks = 4 * prop.multiProcessorCount;
     c->lb_bytes = lb_bytes;
-    c->geom.copy_ctr = (uint64_t *)((uint8_t *)c->lb_dec + lb_bytes - 64);
-    c->geom.copy_base = c->copy_base;
     // clean look-back state: epoch 0 with no published tile. On a stream of
     // the call's own, so work other contexts have in flight keeps running.
     hipStream_t s = nullptr;
@@ -281,7 +277,6 @@ int32_t honu_ctx_reset(honu_ctx *ctx, void *stream) {
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipMemsetAsync(ctx->lb_dec, 0, ctx->lb_bytes, (hipStream_t)stream));
     HIPCHK(hipStreamSynchronize((hipStream_t)stream));
-    for (int k = 0; k < 3; k++) ctx->copy_base[k] = 0;
     return HONU_OK;
 }
 

@@ -21,7 +21,6 @@ namespace honu {
 // Segment i of an encode: src = payload[payload_off[i] ...], logical start =
 // payload_off[i], dst = out + out_off[i] + 1 + uvarint_len(len).
 struct EncodeSegments {
-    static constexpr int KIND = 0;  // ticket counter (LaunchGeom::copy_ctr)
     const uint8_t *payload;
     const uint64_t *payload_off;
     uint8_t *out;
@@ -53,7 +52,6 @@ struct EncodeSegments {
 // Segment i of a materialising decode: logical start = offs[3i+2] (the
 // destination offset), src = rec + scratch[i].data_src.
 struct DecodeSegments {
-    static constexpr int KIND = 1;
     const uint8_t *rec;
     const honu_record_info *info;
     const DecodeScratch *scratch;
@@ -76,7 +74,6 @@ struct DecodeSegments {
 // Segment i of honu_decode_data: logical start = offs[i] (one column, the
 // destination offset), src = rec + scratch[i].data_src.
 struct SpanSegments {
-    static constexpr int KIND = 2;
     const uint8_t *rec;
     const honu_record_info *info;
     const DecodeScratch *scratch;
@@ -148,33 +145,6 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t 
         const uint64_t y = e < hi ? e : hi;
         if (x < y)
             wave_copy<UNROLL, NT>(dst + (x - s), src + (x - s), y - x);
-    }
-}
-
-// Ticket form (long segments): a wave takes whole segments from a counter, so
-// a wave that starts late, or shares its CU with a scan-heavy metadata kernel,
-// copies fewer bytes instead of ending the launch late (the range form fixes
-// every wave's bytes up front). The counter is never reset: a launch over n
-// segments with W waves takes exactly n + W tickets (every wave's last one
-// fails), so the host passes the counter's value at the launch's start.
-template <class Seg, int UNROLL>
-__global__ __launch_bounds__(HONU_BLOCK) void k_copy_tickets(Seg seg, uint64_t n, uint64_t *__restrict__ ctr,
-                                                              uint64_t base) {
-    auto take = [&]() -> uint64_t {
-        uint64_t v = 0;
-        if (lane_id() == 0) v = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return (((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), 0)) << 32 |
-                __builtin_amdgcn_readlane((uint32_t)v, 0)) - base;
-    };
-    uint64_t t = take();
-    while (t < n) {
-        uint64_t len;
-        const uint8_t *src;
-        uint8_t *dst;
-        const bool ok = seg.get(t, len, src, dst);
-        const uint64_t tn = take();  // the next ticket's round trip hides under this copy
-        if (ok) wave_copy<UNROLL, 0>(dst, src, len);
-        t = tn;
     }
 }
 
@@ -257,17 +227,6 @@ static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
             hipLaunchKernelGGL((k_copy_sweep<Seg, 8>), grid, block, 0, s, seg, n, total, g.tile_map, g.tile_map_cap);
         else
             hipLaunchKernelGGL((k_copy_sweep<Seg, 4>), grid, block, 0, s, seg, n, total, g.tile_map, g.tile_map_cap);
-        return hipGetLastError();
-    }
-    if (g.copy_variant == 21 || g.copy_variant == 22) {  // ticket form for long segments
-        const dim3 gt(g.copy_blocks);
-        uint64_t *ctr = g.copy_ctr + Seg::KIND;
-        const uint64_t base = g.copy_base[Seg::KIND];
-        g.copy_base[Seg::KIND] += n + (uint64_t)g.copy_blocks * HONU_WAVES_PER_BLOCK;
-        if (g.copy_variant == 22)
-            hipLaunchKernelGGL((k_copy_tickets<Seg, 8>), gt, block, 0, s, seg, n, ctr, base);
-        else
-            hipLaunchKernelGGL((k_copy_tickets<Seg, 4>), gt, block, 0, s, seg, n, ctr, base);
         return hipGetLastError();
     }
     switch (g.copy_variant) {

@@ -93,9 +93,6 @@ struct LaunchGeom {
                             // per-group / per-lane forms 1-4: DESIGN §3)
     uint32_t *tile_map;     // sweep-form tile -> segment map (context scratch)
     uint64_t tile_map_cap;
-    uint64_t *copy_ctr;     // segment tickets of the ticket-form copies (device, one
-                            // counter per segment kind: encode, decode, span)
-    uint64_t *copy_base;    // (host) each counter's value at the next launch's start
 };
 
 hipError_t launch_encode_copy(const LaunchGeom &g, const uint8_t *payload,
