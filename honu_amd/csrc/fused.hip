@@ -234,6 +234,7 @@ struct AclStage {
 // list's first flag, cnt: its entries, 0 for none) into the wave's LDS, 256
 // bytes per list: instruction k has lane j fetch flag j of lane k's list (a
 // few cache lines per instruction, the lines the list occupies anyway).
+// (lane k's flags in LDS row k, FLAG_ROW apart: win.h)
 HONU_DEV void flag_gather(uint8_t *ws, const uint8_t *__restrict__ rec, uint64_t base, uint64_t cnt,
                           uint64_t from) {
     const uint32_t lane = lane_id();
@@ -247,7 +248,7 @@ HONU_DEV void flag_gather(uint8_t *ws, const uint8_t *__restrict__ rec, uint64_t
         if (lane < mk)
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)(rec + ((bk + 18ull * lane) & ~3ull)),
-                (__attribute__((address_space(3))) void *)(ws + 256 * k), 4, 0, 0);
+                (__attribute__((address_space(3))) void *)(ws + FLAG_ROW * k), 4, 0, 0);
     }
 }
 // After flag_gather(.., 0): true when a flag of this lane's list (chk) is not
@@ -265,7 +266,7 @@ HONU_DEV bool flag_check(uint8_t *ws, const uint8_t *__restrict__ rec, bool chk,
             const uint32_t m = (uint32_t)(cnt - from < HONU_WAVE ? cnt - from : HONU_WAVE);
             const uint64_t b = base + 18 * from;
             const __attribute__((address_space(3))) uint8_t *fl =
-                (const __attribute__((address_space(3))) uint8_t *)(ws + 256 * lane);
+                (const __attribute__((address_space(3))) uint8_t *)(ws + FLAG_ROW * lane);
 #pragma unroll
             for (uint32_t j = 0; j < HONU_WAVE; j++)
                 if (j < m) bad |= fl[4 * j + (uint32_t)((b + 18ull * j) & 3)] != 1;

@@ -42,6 +42,13 @@ constexpr uint32_t WS = WSL * 16;
 constexpr uint64_t NOWIN = ~0ull;
 // windows + per-lane wanted base, previous base and fetch limit
 constexpr uint32_t WIN_WAVE_BYTES = HONU_WAVE * WS + 3 * HONU_WAVE * 8;
+// The ACL flag gathers (the walk below, fused.hip flag_gather): lane k's flags
+// land in LDS row k; rows are 65 dwords apart, so when every lane reads flag j
+// of its own row the 64 reads fall on 64 different banks (with 64-dword rows
+// they all hit bank j, a 64-way conflict per flag: 1M Small zero copy
+// 2.5 % slower, profiles/r05/lds/).
+constexpr uint32_t FLAG_ROW = 4 * (HONU_WAVE + 1);
+static_assert(FLAG_ROW * HONU_WAVE <= WIN_WAVE_BYTES, "the flag rows fit a wave's windows");
 // region ids of a record kept in registers by the walk (the generator writes
 // at most 9); longer lists are re-read from the record by the fill
 constexpr int REG_INLINE = 9;
@@ -477,7 +484,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
             if (lane < __builtin_amdgcn_readlane(gcnt, k))
                 __builtin_amdgcn_global_load_lds(
                     (const __attribute__((address_space(1))) void *)(rec + ((base + 18ull * lane) & ~3ull)),
-                    (__attribute__((address_space(3))) void *)(W.wave + 256 * k), 4, 0, 0);
+                    (__attribute__((address_space(3))) void *)(W.wave + FLAG_ROW * k), 4, 0, 0);
         }
         __builtin_amdgcn_s_waitcnt(0);
         wave_sync();
@@ -485,7 +492,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
         if (fast) {
             const uint32_t m = (uint32_t)(nacl < 64 ? nacl : 64);
             const __attribute__((address_space(3))) uint8_t *fl =
-                (const __attribute__((address_space(3))) uint8_t *)(W.wave + 256 * lane);
+                (const __attribute__((address_space(3))) uint8_t *)(W.wave + FLAG_ROW * lane);
             bool ok = true;
 #pragma unroll
             for (uint32_t j = 0; j < 64; j++)
