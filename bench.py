@@ -376,10 +376,12 @@ class Bench:
         if self.encode_only:
             return self._issue_encode_copy(a, b, sl, sm, timed, ev_off, (o0, o1) if timed else None)
         if self.fused_decode(n):  # parse + look-back + tables in one launch (fused.hip)
-            # with two metadata streams the previous chunk's decode (and its
-            # guarded launch) finishes first: a guard that is a no-op would
-            # otherwise wait up to ~1 ms for LDS this decode's persistent grid
-            # holds, and hold up its stream meanwhile
+            # --decode-chain (default on): with two metadata streams the
+            # previous chunk's decode (and its guarded launch) finishes first,
+            # so the two slots' persistent decodes never share the chip
+            # (measured equal to off: a guard waits for registers the other
+            # slot's tail encoder holds, not for the other decode; DESIGN §3
+            # "Round 5: the guard in one-wave workgroups")
             chain = self.args.decode_chain and len(self.sms) > 1
             dm = sm
             if self.sdec is not None:  # fork onto the slot's high-priority decode stream

@@ -48,3 +48,21 @@ def test_launcher_refuses_missing_gpus():
 def test_world_size_must_match():
     r = _run(["--gpus", "1", "--records", "10"], env=_env(WORLD_SIZE="2", RANK="0"))
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_default_line_legs():
+    """--legs: the default 1M Large encdec line carries configs[1] (small) and
+    configs[3] (mixed_encode); other lines none unless asked; 'none' and
+    unknown legs (no GPU needed: argument handling only)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.legs_of(bench.parse_args([])) == ["small", "mixed_encode"]
+    assert bench.legs_of(bench.parse_args(["--legs", "none"])) == []
+    assert bench.legs_of(bench.parse_args(["--shape", "small"])) == []
+    assert bench.legs_of(bench.parse_args(["--records", "1000"])) == []
+    assert bench.legs_of(bench.parse_args(["--mode", "decode"])) == []
+    assert bench.legs_of(bench.parse_args(["--shape", "medium", "--legs", "small"])) == ["small"]
+    with pytest.raises(SystemExit):
+        bench.legs_of(bench.parse_args(["--legs", "small,bogus"]))
+    # the legs' configurations: Small encode + decode, Mixed encode only
+    assert bench.LEG_SHAPES == {"small": ("small", False), "mixed_encode": ("mixed", True)}

@@ -126,6 +126,40 @@ def test_bench_copy_order_ahead(oracle_lib, shape, n, slots):
     assert b.verify()
 
 
+@pytest.mark.parametrize("shape,n", [("mixed", 1500), ("small", 4000)])
+def test_bench_encode_only_bit_exact(oracle_lib, shape, n):
+    """--mode encode (configs[3]: size pass, scan, header/tail encoder and
+    payload copy, no decode), the pipeline the default line's mixed_encode
+    leg times: every chunk's records equal oracle.marshal_batch's, and the
+    bench's own verification (zero-copy decode of each chunk, row and payload
+    digests) passes."""
+    seed = 5
+    args = bench.parse_args(["--records", str(n), "--shape", shape, "--min-chunks", "4",
+                             "--seed", str(seed), "--mode", "encode"])
+    b = bench.Bench(args, 0, 0, encode_only=True)
+    assert len(b.chunks) >= 4
+    hb = gen_host_batch(seed, shape, 0, n)
+    seen = []
+
+    def check(a, z, sl):
+        sub = HostBatch(hb.meta[a:z], hb.var, hb.acl, hb.regions, hb.payload,
+                        hb.payload_off[a:z + 1])
+        oout, ooff, ost = oracle_lib.marshal_batch(sub)
+        assert np.array_equal(_host(sl.status, 4 * (z - a), np.int32), ost)
+        assert np.array_equal(_host(sl.out_off, 8 * (z - a + 1), np.uint64), ooff)
+        assert _host(sl.out, int(ooff[-1])).tobytes() == oout.tobytes(), (a, z)
+        seen.append((a, z))
+        return True
+
+    for _ in range(2):
+        b.step()
+    for _ in range(2):
+        assert b.step(check=check)
+    torch.cuda.synchronize()
+    assert seen == b.chunks * 2
+    assert b.verify()
+
+
 def test_bench_verify_detects_corruption():
     """_verify_chunk (honu_verify_decoded + digests) flags one wrong byte in a
     decoded ObjectID, span, ACL entry (in place in the records arena: its
