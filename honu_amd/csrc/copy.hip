@@ -99,9 +99,39 @@ struct SpanSegments {
 #define COPY_FEW_WAVES_MIN (64u << 10)
 #endif
 
-template <class Seg, int UNROLL, int NT>
+// TWO (the default; variant 40 of the A/B build without it): a launch of long
+// segments on average (>= COPY_FEW_WAVES_MIN) gives its first 1 /
+// SMALL_SEG_WAVES_FACTOR of waves the long segments (byte ranges as below,
+// short segments skipped) and the other waves, which used to return at once,
+// the short ones (each wave a range of segment indices, short segments
+// whole): the short records of a mixed batch no longer hold up the few
+// streaming waves. 1M Mixed encode + decode 1238-1248 -> 1266-1268 GiB/s on
+// one box, 1152-1176 -> 1189-1230 on another (interleaved; every Large and
+// XLarge payload is >= 64 KB, so those batches have no short class, and they
+// measured equal within the runs' order effect; profiles/r05/copy_classes/).
+// (Every wave on every segment instead: Mixed 7 % slower, the long segments'
+// streams too many.)
+template <class Seg, int UNROLL>
+HONU_DEV void copy_short_class(const Seg &seg, uint64_t n, uint64_t v, uint64_t V, uint64_t short_max) {
+    const uint64_t i0 = n * v / V, i1 = n * (v + 1) / V;
+    uint64_t len_nx = 0;
+    const uint8_t *src_nx = nullptr;
+    uint8_t *dst_nx = nullptr;
+    bool ok_nx = i0 < i1 && seg.get(i0, len_nx, src_nx, dst_nx);
+    for (uint64_t i = i0; i < i1; i++) {
+        const uint64_t len = len_nx;
+        const uint8_t *src = src_nx;
+        uint8_t *dst = dst_nx;
+        const bool ok = ok_nx;
+        if (i + 1 < i1) ok_nx = seg.get(i + 1, len_nx, src_nx, dst_nx);
+        if (ok && len < short_max) wave_copy<UNROLL, 0>(dst, src, len);
+    }
+}
+
+template <class Seg, int UNROLL, int NT, bool TWO = false>
 __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t n,
-                                                               const uint64_t *__restrict__ total_p) {
+                                                               const uint64_t *__restrict__ total_p,
+                                                               uint64_t short_max = COPY_FEW_WAVES_MIN) {
     uint64_t W = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
     const uint64_t w = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + wave_in_block();
     const uint64_t base = seg.lo();
@@ -109,7 +139,17 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t 
     // Large segments stream best from few waves (DRAM rows stay open: 2 WG per
     // CU measured best); short segments are latency bound and want every wave
     // the launch has (SMALL_SEG_WAVES_FACTOR x more).
-    if (n && total / n >= COPY_FEW_WAVES_MIN) W /= SMALL_SEG_WAVES_FACTOR;
+    const bool few = n && total / n >= COPY_FEW_WAVES_MIN;
+    if (few) {
+        const uint64_t Wall = W;
+        W /= SMALL_SEG_WAVES_FACTOR;
+        if constexpr (TWO) {
+            if (w >= W) {
+                copy_short_class<Seg, UNROLL>(seg, n, w - W, Wall - W, short_max);
+                return;
+            }
+        }
+    }
     if (w >= W) return;
     const uint64_t lo = base + ((total * w / W) & ~15ull);
     const uint64_t hi = (w + 1 == W) ? base + total : base + ((total * (w + 1) / W) & ~15ull);
@@ -140,6 +180,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t 
             ok_nx = seg.get(i + 1, len_nx, src_nx, dst_nx);
         }
         if (!ok) continue;
+        if (TWO && few && len < short_max) continue;  // the short class's
         const uint64_t x = s > lo ? s : lo;
         const uint64_t e = s + len;
         const uint64_t y = e < hi ? e : hi;
@@ -212,8 +253,9 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_sweep(Seg seg, uint64_t n,
 // Copy-engine variants (A/B build only, tools/tune_copy.py): 1-5 contiguous
 // per-wave ranges {unroll, non-temporal}; 6-7 the sweep form; 11 / 12
 // non-temporal loads only / stores only; 13-15 one unaligned 16-byte load per
-// chunk instead of two aligned loads and a funnel. The product library has
-// variant 0 only (unroll 4, default cache policy: measured fastest).
+// chunk instead of two aligned loads and a funnel; 40 without the short-
+// segment class. The product library has variant 0 only (unroll 4, default
+// cache policy, two segment classes: measured fastest).
 template <class Seg>
 static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
                               const uint64_t *total, hipStream_t s) {
@@ -240,10 +282,18 @@ static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
     case 13: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 4>), grid, block, 0, s, seg, n, total); return hipGetLastError();
     case 14: hipLaunchKernelGGL((k_copy_segments<Seg, 8, 4>), grid, block, 0, s, seg, n, total); return hipGetLastError();
     case 15: hipLaunchKernelGGL((k_copy_segments<Seg, 2, 4>), grid, block, 0, s, seg, n, total); return hipGetLastError();
+    case 40: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0, false>), grid, block, 0, s, seg, n, total); return hipGetLastError();
+    case 42: {  // the short class's bound from the environment (bytes)
+        static const uint64_t sm = getenv("HONU_COPY_SHORT_MAX") ? strtoull(getenv("HONU_COPY_SHORT_MAX"), nullptr, 10)
+                                                                 : (uint64_t)COPY_FEW_WAVES_MIN;
+        hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0, true>), grid, block, 0, s, seg, n, total, sm);
+        return hipGetLastError();
+    }
     default: break;
     }
 #endif
-    hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0>), grid, block, 0, s, seg, n, total);
+    hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0, true>), grid, block, 0, s, seg, n, total,
+                       (uint64_t)COPY_FEW_WAVES_MIN);
     return hipGetLastError();
 }
 
