@@ -323,9 +323,10 @@ struct SpecPub {
 // maybe from another XCD, must land after them), counts its tiles into
 // rdone, and once all are released the waves decode the batch again without
 // speculation from a second ticket counter, with look-back words tagged as
-// pass 1 (lookback.h). No launch waits for a CU with 78 KB of free LDS
-// behind other kernels (a guard launch that was a no-op
-// spent up to 1.4 ms queued beside the bench's copies and encoder). Static
+// pass 1 (lookback.h). No second launch waits for CU resources behind other
+// kernels (a no-op guard of 78 KB workgroups spent up to
+// 1.4 ms queued beside the bench's copies and encoder; the guard is now
+// k_decode_guard below). Measured slower in the clean case, so off. Static
 // tiles keep the guarded launch: their waves may wait on workgroups that are
 // not resident yet, so a launch-wide wait could deadlock beside another
 // persistent kernel.

@@ -244,9 +244,9 @@ int32_t honu_ctx_reset(honu_ctx *ctx, void *stream);
  * of copying it into the ACL table; 0 returns every list in the table.
  * "inline_recovery" (0 default, 1 on): a speculative single-launch decode
  * with more 64-record tiles than resident waves redoes a misspeculated batch
- * inside the same launch instead of in a guarded second launch (whose 78 KB
- * LDS workgroups can queue behind other kernels even when it has nothing to
- * do); launches whose tiles all fit keep the guarded launch. Measured slower
+ * inside the same launch instead of in a guarded second launch (one-wave
+ * workgroups, placed as registers free up beside other kernels even when it
+ * has nothing to do); launches whose tiles all fit keep the guarded launch. Measured slower
  * in the common, clean case (DESIGN §3 "Round 5"), hence off. "recoveries"
  * (get only): the recovery passes or launches the context has run. */
 int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value);
