@@ -123,6 +123,11 @@ def parse_args(argv=None):
                    help="chunk: a chunk's decode copy right after its encode copy on the copy stream; "
                         "ahead: after the NEXT chunk's encode copy, so the copy stream does not wait "
                         "for a chunk's Metadata decode")
+    p.add_argument("--enc-units", type=int, default=1, choices=[0, 1],
+                   help="1: the payload-unit encode pair (honu_encode_records_units + "
+                        "honu_encode_payloads_units: the encoder writes each payload's partial end "
+                        "64-byte units, the copy the whole ones); 0: honu_encode_records + "
+                        "honu_encode_payloads")
     p.add_argument("--decode-chain", type=int, default=1, choices=[0, 1],
                    help="with two metadata streams, a chunk's single-launch decode waits for the "
                         "previous chunk's (and its guarded launch): the guard never queues for "
@@ -283,6 +288,7 @@ class Bench:
         # --copy-order ahead: the last chunk's decode copy, issued after the
         # next chunk's encode copy (flush() issues it)
         self.ahead = getattr(args, "copy_order", "chunk") == "ahead" and nslots >= 2 and not encode_only
+        self.units = bool(getattr(args, "enc_units", 1))  # the payload-unit encode pair
         self.pending_dec = None
         torch.cuda.synchronize()
 
@@ -366,10 +372,16 @@ class Bench:
         ev_off.record(sm)
         if timed and self.encode_only:
             o1.record(sm)
-        _lib.check(L.honu_encode_records(c, P(self.meta) + 352 * a, P(self.var), P(self.acl),
-                                         P(self.reg), P(self.off) + 8 * a, n, P(sl.out),
-                                         self.out_cap, P(sl.out_off), P(sl.status), ms),
-                   "encode_records")
+        if self.units:  # the encoder also writes the payloads' partial end 64-byte units
+            _lib.check(L.honu_encode_records_units(c, P(self.meta) + 352 * a, P(self.var), P(self.acl),
+                                                   P(self.reg), P(self.payload), P(self.off) + 8 * a, n,
+                                                   P(sl.out), self.out_cap, P(sl.out_off), P(sl.status), ms),
+                       "encode_records_units")
+        else:
+            _lib.check(L.honu_encode_records(c, P(self.meta) + 352 * a, P(self.var), P(self.acl),
+                                             P(self.reg), P(self.off) + 8 * a, n, P(sl.out),
+                                             self.out_cap, P(sl.out_off), P(sl.status), ms),
+                       "encode_records")
         if self.args.encode_copy_after == "meta":
             ev_off = torch.cuda.Event()
             ev_off.record(sm)
@@ -417,9 +429,10 @@ class Bench:
         e1 = torch.cuda.Event(enable_timing=True) if timed else None
         if timed:
             e0.record(sc)
-        _lib.check(L.honu_encode_payloads(c, P(self.payload), P(self.off) + 8 * a, n,
-                                          P(sl.out), self.out_cap, P(sl.out_off), P(sl.status),
-                                          cs), "encode_payloads")
+        enc_copy = L.honu_encode_payloads_units if self.units else L.honu_encode_payloads
+        _lib.check(enc_copy(c, P(self.payload), P(self.off) + 8 * a, n,
+                            P(sl.out), self.out_cap, P(sl.out_off), P(sl.status),
+                            cs), "encode_payloads")
         if timed:
             e1.record(sc)
         self.enc_done = torch.cuda.Event()
@@ -461,9 +474,10 @@ class Bench:
         e1 = torch.cuda.Event(enable_timing=True) if timed else None
         if timed:
             e0.record(sc)
-        _lib.check(L.honu_encode_payloads(sl.codec.ctx, P(self.payload), P(self.off) + 8 * a, n,
-                                          P(sl.out), self.out_cap, P(sl.out_off), P(sl.status),
-                                          sc.cuda_stream), "encode_payloads")
+        enc_copy = L.honu_encode_payloads_units if self.units else L.honu_encode_payloads
+        _lib.check(enc_copy(sl.codec.ctx, P(self.payload), P(self.off) + 8 * a, n,
+                            P(sl.out), self.out_cap, P(sl.out_off), P(sl.status),
+                            sc.cuda_stream), "encode_payloads")
         if timed:
             e1.record(sc)
             self.events.append((a, b, e0, e1) + tuple(off_events))

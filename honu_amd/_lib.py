@@ -40,6 +40,8 @@ _PROTOS = {
     "honu_encode": (I32, [P, P, P, U64, P, U64, P, U64, P, P, U64, P, U64, P, P, P]),
     "honu_encode_records": (I32, [P, P, P, P, P, P, U64, P, U64, P, P, P]),
     "honu_encode_payloads": (I32, [P, P, P, U64, P, U64, P, P, P]),
+    "honu_encode_records_units": (I32, [P, P, P, P, P, P, P, U64, P, U64, P, P, P]),
+    "honu_encode_payloads_units": (I32, [P, P, P, U64, P, U64, P, P, P]),
     "honu_decode_tables": (I32, [P, P, U64, P, P, P, U64, P, U64, P, U64, P, P]),
     "honu_decode_payloads": (I32, [P, P, U64, P, P, P, P]),
     "honu_marshal_batch": (I32, [P, P, P, U64, P, U64, P, U64, P, P, U64, P, U64, P, P, P]),

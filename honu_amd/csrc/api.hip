@@ -366,11 +366,12 @@ int32_t honu_exclusive_scan(honu_ctx *ctx, const uint64_t *d_in, uint64_t n, uin
     return HONU_OK;
 }
 
-int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
-                            const honu_acl *d_acl, const uint32_t *d_regions,
-                            const uint64_t *d_payload_off, uint64_t n, uint8_t *d_out,
-                            uint64_t out_cap, const uint64_t *d_out_off, int32_t *d_status,
-                            void *stream) {
+// units: the payload arena (honu_encode_records_units), or null
+static int32_t encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
+                              const honu_acl *d_acl, const uint32_t *d_regions, const uint8_t *units,
+                              const uint64_t *d_payload_off, uint64_t n, uint8_t *d_out,
+                              uint64_t out_cap, const uint64_t *d_out_off, int32_t *d_status,
+                              void *stream) {
     if (!ctx) return arg_fail("ctx");
     if (n && (!d_meta || !d_payload_off || !d_out || !d_out_off || !d_status))
         return arg_fail("null pointer");
@@ -378,7 +379,7 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
     HIPCHK(hipSetDevice(ctx->device));
     if (n > ctx->max_n) return HONU_E_WORKSPACE;
 #ifdef HONU_AB
-    if (ctx->geom.encode_variant == 1) {  // one launch, 16 lanes per record (enc.hip, A/B build only)
+    if (ctx->geom.encode_variant == 1 && !units) {  // one launch, 16 lanes per record (enc.hip, A/B build only)
         HIPCHK(launch_encode_tail_grp(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
                                       out_cap, d_out_off, d_status, ctx->geom.lane_blocks,
                                       (hipStream_t)stream));
@@ -405,27 +406,58 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
         HIPCHK(hipEventRecord(ctx->ev_join, ctx->aux));
         HIPCHK(launch_encode_meta_lane(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
                                        out_cap, d_out_off, d_status, ctx->enc_acl,
-                                       ctx->geom.lane_blocks, ctx->geom.num_cu, s));
+                                       ctx->geom.lane_blocks, ctx->geom.num_cu, units, s));
         HIPCHK(hipStreamWaitEvent(s, ctx->ev_join, 0));
         return HONU_OK;
     }
     HIPCHK(launch_encode_meta_lane(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
                                    out_cap, d_out_off, d_status, ctx->enc_acl,
-                                   ctx->geom.lane_blocks, ctx->geom.num_cu, s));
+                                   ctx->geom.lane_blocks, ctx->geom.num_cu, units, s));
     HIPCHK(launch_encode_acl_grp(d_meta, d_acl, n, d_out, d_status, ctx->enc_acl,
                                  ctx->geom.lane_blocks, s));
+    return HONU_OK;
+}
+
+int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
+                            const honu_acl *d_acl, const uint32_t *d_regions,
+                            const uint64_t *d_payload_off, uint64_t n, uint8_t *d_out,
+                            uint64_t out_cap, const uint64_t *d_out_off, int32_t *d_status,
+                            void *stream) {
+    return encode_records(ctx, d_meta, d_var, d_acl, d_regions, nullptr, d_payload_off, n, d_out, out_cap,
+                          d_out_off, d_status, stream);
+}
+
+int32_t honu_encode_records_units(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
+                                  const honu_acl *d_acl, const uint32_t *d_regions,
+                                  const uint8_t *d_payload, const uint64_t *d_payload_off, uint64_t n,
+                                  uint8_t *d_out, uint64_t out_cap, const uint64_t *d_out_off,
+                                  int32_t *d_status, void *stream) {
+    if (n && !d_payload) return arg_fail("null pointer");
+    return encode_records(ctx, d_meta, d_var, d_acl, d_regions, d_payload, d_payload_off, n, d_out, out_cap,
+                          d_out_off, d_status, stream);
+}
+
+static int32_t encode_payloads(honu_ctx *ctx, const uint8_t *d_payload, const uint64_t *d_payload_off,
+                               uint64_t n, uint8_t *d_out, uint64_t out_cap, const uint64_t *d_out_off,
+                               const int32_t *d_status, bool units, void *stream) {
+    if (!ctx) return arg_fail("ctx");
+    if (n && (!d_payload_off || !d_out || !d_out_off || !d_status)) return arg_fail("null pointer");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_encode_copy(ctx->geom, d_payload, d_payload_off, n, d_out, out_cap, d_out_off,
+                              d_status, units, (hipStream_t)stream));
     return HONU_OK;
 }
 
 int32_t honu_encode_payloads(honu_ctx *ctx, const uint8_t *d_payload, const uint64_t *d_payload_off,
                              uint64_t n, uint8_t *d_out, uint64_t out_cap, const uint64_t *d_out_off,
                              const int32_t *d_status, void *stream) {
-    if (!ctx) return arg_fail("ctx");
-    if (n && (!d_payload_off || !d_out || !d_out_off || !d_status)) return arg_fail("null pointer");
-    HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(launch_encode_copy(ctx->geom, d_payload, d_payload_off, n, d_out, out_cap, d_out_off,
-                              d_status, (hipStream_t)stream));
-    return HONU_OK;
+    return encode_payloads(ctx, d_payload, d_payload_off, n, d_out, out_cap, d_out_off, d_status, false, stream);
+}
+
+int32_t honu_encode_payloads_units(honu_ctx *ctx, const uint8_t *d_payload, const uint64_t *d_payload_off,
+                                   uint64_t n, uint8_t *d_out, uint64_t out_cap, const uint64_t *d_out_off,
+                                   const int32_t *d_status, void *stream) {
+    return encode_payloads(ctx, d_payload, d_payload_off, n, d_out, out_cap, d_out_off, d_status, true, stream);
 }
 
 int32_t honu_encode(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var, uint64_t var_len,
@@ -436,11 +468,12 @@ int32_t honu_encode(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var
     (void)var_len;
     (void)acl_len;
     (void)regions_len;
-    int32_t st = honu_encode_records(ctx, d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
-                                     out_cap, d_out_off, d_status, stream);
+    // the payload-unit pair (one kernel per 64-byte unit of the output)
+    int32_t st = honu_encode_records_units(ctx, d_meta, d_var, d_acl, d_regions, d_payload, d_payload_off, n,
+                                           d_out, out_cap, d_out_off, d_status, stream);
     if (st) return st;
-    return honu_encode_payloads(ctx, d_payload, d_payload_off, n, d_out, out_cap, d_out_off,
-                                d_status, stream);
+    return honu_encode_payloads_units(ctx, d_payload, d_payload_off, n, d_out, out_cap, d_out_off,
+                                      d_status, stream);
 }
 
 int32_t honu_marshal_batch(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,

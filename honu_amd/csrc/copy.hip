@@ -34,7 +34,8 @@ struct EncodeSegments {
         (void)total_abs;
         return payload_off[i + 1];
     }
-    HONU_DEV bool get(uint64_t i, uint64_t &len, const uint8_t *&src, uint8_t *&dst) const {
+    bool units;  // honu_encode_payloads_units: the encoder wrote the payload's partial end 64-byte units
+    HONU_DEV bool get(uint64_t i, uint64_t &len, const uint8_t *&src, uint8_t *&dst, uint64_t &skip) const {
         // the header/tail encoder may still be running on another stream:
         // its HONU_ERR_CAPACITY is not visible here, so the capacity check
         // is repeated (nothing is written past out_cap)
@@ -45,6 +46,17 @@ struct EncodeSegments {
         len = payload_off[i + 1] - s;
         src = payload + s;
         dst = out + o0 + 1 + uvarint_len(len);
+        skip = 0;
+        if (units) {  // the same units as lane.h encode_record_lane (absolute addresses)
+            const uint64_t a0 = (uint64_t)dst, a1 = a0 + len;
+            const uint64_t h_end = ((a0 + PAYLOAD_UNIT - 1) & ~(PAYLOAD_UNIT - 1)) < a1
+                                       ? ((a0 + PAYLOAD_UNIT - 1) & ~(PAYLOAD_UNIT - 1)) : a1;
+            const uint64_t t_beg = (a1 & ~(PAYLOAD_UNIT - 1)) > h_end ? (a1 & ~(PAYLOAD_UNIT - 1)) : h_end;
+            skip = h_end - a0;
+            len = t_beg - h_end;
+            src += skip;
+            dst += skip;
+        }
         return st == HONU_OK && o1 <= out_cap && len != 0;
     }
 };
@@ -62,7 +74,8 @@ struct DecodeSegments {
     HONU_DEV uint64_t lo() const { return 0; }
     HONU_DEV uint64_t end(uint64_t i, uint64_t total_abs) const { return i + 1 < n_ ? offs[3 * i + 5] : total_abs; }
     uint64_t n_;
-    HONU_DEV bool get(uint64_t i, uint64_t &len, const uint8_t *&src, uint8_t *&dst) const {
+    HONU_DEV bool get(uint64_t i, uint64_t &len, const uint8_t *&src, uint8_t *&dst, uint64_t &skip) const {
+        skip = 0;
         const int32_t st = info[i].data_status;  // every field in one round trip
         len = info[i].data_len;
         src = rec + scratch[i].data_src;
@@ -83,7 +96,8 @@ struct SpanSegments {
     HONU_DEV uint64_t start(uint64_t i) const { return offs[i]; }
     HONU_DEV uint64_t lo() const { return 0; }
     HONU_DEV uint64_t end(uint64_t i, uint64_t total_abs) const { (void)total_abs; return offs[i + 1]; }
-    HONU_DEV bool get(uint64_t i, uint64_t &len, const uint8_t *&src, uint8_t *&dst) const {
+    HONU_DEV bool get(uint64_t i, uint64_t &len, const uint8_t *&src, uint8_t *&dst, uint64_t &skip) const {
+        skip = 0;
         const int32_t st = info[i].data_status;  // every field in one round trip
         len = info[i].data_len;
         src = rec + scratch[i].data_src;
@@ -114,16 +128,16 @@ struct SpanSegments {
 template <class Seg, int UNROLL>
 HONU_DEV void copy_short_class(const Seg &seg, uint64_t n, uint64_t v, uint64_t V, uint64_t short_max) {
     const uint64_t i0 = n * v / V, i1 = n * (v + 1) / V;
-    uint64_t len_nx = 0;
+    uint64_t len_nx = 0, skip = 0;
     const uint8_t *src_nx = nullptr;
     uint8_t *dst_nx = nullptr;
-    bool ok_nx = i0 < i1 && seg.get(i0, len_nx, src_nx, dst_nx);
+    bool ok_nx = i0 < i1 && seg.get(i0, len_nx, src_nx, dst_nx, skip);
     for (uint64_t i = i0; i < i1; i++) {
         const uint64_t len = len_nx;
         const uint8_t *src = src_nx;
         uint8_t *dst = dst_nx;
         const bool ok = ok_nx;
-        if (i + 1 < i1) ok_nx = seg.get(i + 1, len_nx, src_nx, dst_nx);
+        if (i + 1 < i1) ok_nx = seg.get(i + 1, len_nx, src_nx, dst_nx, skip);
         if (ok && len < short_max) wave_copy<UNROLL, 0>(dst, src, len);
     }
 }
@@ -165,19 +179,21 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t 
     // loaded one segment ahead: issued before the current segment's copy, they
     // arrive with its loads, so a short segment costs one round trip instead
     // of three (start -> descriptors -> bytes).
-    uint64_t s_nx = seg.start(a), len_nx = 0;
+    // (skip: the segment's copy starts that many bytes into it, EncodeSegments
+    // with units; its logical range is then [start + skip, + len))
+    uint64_t s_nx = seg.start(a), len_nx = 0, skip_nx = 0;
     const uint8_t *src_nx = nullptr;
     uint8_t *dst_nx = nullptr;
-    bool ok_nx = seg.get(a, len_nx, src_nx, dst_nx);
+    bool ok_nx = seg.get(a, len_nx, src_nx, dst_nx, skip_nx);
     for (uint64_t i = a; i < n; i++) {
-        const uint64_t s = s_nx, len = len_nx;
+        const uint64_t s0 = s_nx, len = len_nx, s = s0 + skip_nx;
         const uint8_t *src = src_nx;
         uint8_t *dst = dst_nx;
         const bool ok = ok_nx;
-        if (s >= hi) break;
+        if (s0 >= hi) break;
         if (i + 1 < n) {
             s_nx = seg.start(i + 1);
-            ok_nx = seg.get(i + 1, len_nx, src_nx, dst_nx);
+            ok_nx = seg.get(i + 1, len_nx, src_nx, dst_nx, skip_nx);
         }
         if (!ok) continue;
         if (TWO && few && len < short_max) continue;  // the short class's
@@ -234,12 +250,14 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_sweep(Seg seg, uint64_t n,
         const uint64_t lo = base + t * T;
         const uint64_t hi = lo + T < base + total ? lo + T : base + total;
         for (uint64_t i = map[t]; i < n; i++) {
-            const uint64_t s = seg.start(i);
+            uint64_t s = seg.start(i);
             if (s >= hi) break;
             uint64_t len;
             const uint8_t *src;
             uint8_t *dst;
-            if (!seg.get(i, len, src, dst)) continue;
+            uint64_t skip;
+            if (!seg.get(i, len, src, dst, skip)) continue;
+            s += skip;
             const uint64_t x = s > lo ? s : lo;
             const uint64_t e = s + len;
             const uint64_t y = e < hi ? e : hi;
@@ -300,9 +318,9 @@ static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
 hipError_t launch_encode_copy(const LaunchGeom &g, const uint8_t *payload,
                               const uint64_t *payload_off, uint64_t n, uint8_t *out,
                               uint64_t out_cap, const uint64_t *out_off, const int32_t *status,
-                              hipStream_t s) {
+                              bool units, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    EncodeSegments seg{payload, payload_off, out, out_cap, out_off, status};
+    EncodeSegments seg{payload, payload_off, out, out_cap, out_off, status, units};
     return launch_copy(g, seg, n, payload_off + n, s);
 }
 

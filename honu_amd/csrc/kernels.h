@@ -31,6 +31,12 @@ struct DecodeScratch {
 // list's partial end chunks are already written (the group kernel stores the
 // whole chunks in between).
 #define ACL_ALL_PRESENT (1ull << 63)
+// The memory side's write unit: a 64-byte unit that leaves L2 partly written
+// costs a read-modify-write (tools/partial_write_probe.hip). The units form of
+// the encode (honu_encode_*_units): the encoder writes a payload's partial end
+// units, the copy the whole ones (lane.h encode_record_lane, copy.hip
+// EncodeSegments).
+#define PAYLOAD_UNIT 64ull
 
 // 01 | ClientID | Permissions, the 18 encoded bytes of a present
 // *AccessControl (acls.go:26-39), as 4.5 little-endian words.
@@ -98,7 +104,7 @@ struct LaunchGeom {
 hipError_t launch_encode_copy(const LaunchGeom &g, const uint8_t *payload,
                               const uint64_t *payload_off, uint64_t n, uint8_t *out,
                               uint64_t out_cap, const uint64_t *out_off, const int32_t *status,
-                              hipStream_t s);
+                              bool units, hipStream_t s);
 
 hipError_t launch_decode_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t n,
                               const honu_record_info *info, const DecodeScratch *scratch,
@@ -114,7 +120,7 @@ hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, co
                                    const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
                                    uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
                                    int32_t *status, uint64_t *acl_out, int max_blocks, int num_cu,
-                                   hipStream_t s);
+                                   const uint8_t *payload, hipStream_t s);
 hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uint64_t n,
                                  uint8_t *out, const int32_t *status, const uint64_t *acl_pos,
                                  int max_blocks, hipStream_t s);

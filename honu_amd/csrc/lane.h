@@ -487,12 +487,19 @@ HONU_DEV uint64_t encode_tail_bytes_noacl(const honu_meta &m, const uint32_t *__
 // (< 8 chunks): between two drains at most one raw-run batch (64 bytes, run()
 // drains before each) plus fixed fields of <= 48 bytes, or <= 96 bytes of
 // fixed fields (uvarints counted at their 10-byte maximum).
+// psrc (honu_encode_records_units): the record's payload bytes; this lane
+// then also writes the payload's bytes in its first and last partial 64-byte
+// units of the output (PAYLOAD_UNIT), so that the copy (EncodeSegments with
+// units) writes whole units only: a 64-byte unit written partly by two
+// kernels at different times costs the memory side a read-modify-write
+// (DESIGN §3 "the 64-byte write unit"). A compile-time null psrc (the plain
+// form's kernel) carries none of it.
 template <bool SKIP_ACL, int R>
 HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restrict__ var,
                                      const honu_acl *__restrict__ acl,
                                      const uint32_t *__restrict__ reg, uint64_t dlen,
                                      uint64_t beg, uint64_t end, uint8_t *__restrict__ out,
-                                     u32x4 *ring) {
+                                     u32x4 *ring, const uint8_t *__restrict__ psrc = nullptr) {
     static_assert(R == 0 || ((R == 8 || R == 16) && SKIP_ACL),
                   "drain spacing assumes 8 slots (16 with line drains: <= 7 held + <= 7 new) and no ACL entries");
 #define OFF(f) ((int)offsetof(honu_meta, f))
@@ -500,16 +507,28 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
     ESTAMP(1);  // row loaded
     const uint8_t *mb = reinterpret_cast<const uint8_t *>(&m);
     const uint32_t pr = m.present;
-    {  // header: version byte + uvarint(len data)   object.go:30,35
+    LaneWriterT<R> W;
+    W.set_ring(ring);
+    if (psrc) {  // header, then the payload's bytes in its partial end units
+        W.init(out, beg);
+        W.byte(HONU_STORAGE_VERSION);
+        W.uv(dlen);
+        const uint64_t a0 = (uint64_t)out + W.pos(), a1 = a0 + dlen;  // absolute payload range
+        const uint64_t h_end = ((a0 + PAYLOAD_UNIT - 1) & ~(PAYLOAD_UNIT - 1)) < a1
+                                   ? ((a0 + PAYLOAD_UNIT - 1) & ~(PAYLOAD_UNIT - 1)) : a1;
+        const uint64_t t_beg = (a1 & ~(PAYLOAD_UNIT - 1)) > h_end ? (a1 & ~(PAYLOAD_UNIT - 1)) : h_end;
+        W.run(psrc, h_end - a0);
+        if (t_beg > h_end) W.jump(t_beg - (uint64_t)out);
+        W.run(psrc + (t_beg - a0), a1 - t_beg);
+        W.drain();
+    } else {  // header: version byte + uvarint(len data)   object.go:30,35
         uint64_t lo, hi;
         const uint32_t hn = uvarint_bytes(dlen, lo, hi);
         out[beg] = HONU_STORAGE_VERSION;
         for (uint32_t j = 0; j < hn; j++)
             out[beg + 1 + j] = (uint8_t)(j < 8 ? lo >> (8 * j) : hi >> (8 * (j - 8)));
+        W.init(out, beg + 1 + uvarint_len(dlen) + dlen);
     }
-    LaneWriterT<R> W;
-    W.init(out, beg + 1 + uvarint_len(dlen) + dlen);
-    W.set_ring(ring);
     W.byte(1);                                                      // EncodeStruct(meta)
     W.put16(ld64(mb + OFF(object_id)), ld64(mb + OFF(object_id) + 8));          // :110
     W.put16(ld64(mb + OFF(collection_id)), ld64(mb + OFF(collection_id) + 8));  // :115

@@ -33,7 +33,7 @@ HONU_DEV void k_encode_meta_lane_one(uint64_t i, const honu_meta &m, const uint8
     const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
     const uint64_t *__restrict__ payload_off, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status,
-    uint64_t *__restrict__ acl_out, u32x4 *ring) {
+    uint64_t *__restrict__ acl_out, u32x4 *ring, const uint8_t *__restrict__ payload) {
     if (status[i] != HONU_OK) return;
     const uint64_t beg = out_off[i], end = out_off[i + 1];
     if (end > out_cap) {
@@ -41,8 +41,8 @@ HONU_DEV void k_encode_meta_lane_one(uint64_t i, const honu_meta &m, const uint8
         return;
     }
     const uint64_t dlen = payload_off[i + 1] - payload_off[i];
-    const uint64_t pos = encode_record_lane<SKIP_ACL, SKIP_ACL ? RING : 0>(m, var, acl, reg, dlen, beg, end,
-                                                                       out, ring);
+    const uint64_t pos = encode_record_lane<SKIP_ACL, SKIP_ACL ? RING : 0>(
+        m, var, acl, reg, dlen, beg, end, out, ring, payload ? payload + payload_off[i] : nullptr);
     if constexpr (SKIP_ACL) acl_out[i] = pos;
 }
 
@@ -55,13 +55,13 @@ HONU_DEV void load_row(const honu_meta *__restrict__ src, honu_meta &m) {
     for (int k = 0; k < 22; k++) d[k] = s[k];
 }
 
-template <bool SKIP_ACL, int RING>
+template <bool SKIP_ACL, int RING, bool UNITS = false>
 __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
     const honu_meta *__restrict__ meta, const uint8_t *__restrict__ var,
     const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
     const uint64_t *__restrict__ payload_off, uint64_t n, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status,
-    uint64_t *__restrict__ acl_out) {
+    uint64_t *__restrict__ acl_out, const uint8_t *__restrict__ payload) {
     constexpr uint32_t WAVE_BYTES = enc_wave_bytes<RING>();
     __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * WAVE_BYTES];
     uint8_t *area = smem + (threadIdx.x / HONU_WAVE) * WAVE_BYTES;
@@ -75,7 +75,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
         if (i < n) {
             load_row(meta + i, m);
             k_encode_meta_lane_one<SKIP_ACL, RING>(i, m, var, acl, reg, payload_off, out, out_cap, out_off, status,
-                                             acl_out, ring);
+                                             acl_out, ring, UNITS ? payload : nullptr);
         }
     }
 }
@@ -198,7 +198,7 @@ hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, co
                                    const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
                                    uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
                                    int32_t *status, uint64_t *acl_out, int max_blocks, int num_cu,
-                                   hipStream_t s) {
+                                   const uint8_t *payload, hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (!acl_out) return hipErrorInvalidValue;
     const dim3 grid = lane_grid(n, max_blocks);
@@ -209,12 +209,15 @@ hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, co
     const uint64_t resident_blocks = grid.x < 2u * (uint64_t)num_cu ? grid.x : 2u * (uint64_t)num_cu;
     const uint64_t line_min_tiles = HONU_WAVES_PER_BLOCK * resident_blocks;
 #endif
-    if ((n + HONU_WAVE - 1) / HONU_WAVE > line_min_tiles)
-        hipLaunchKernelGGL((k_encode_meta_lane<true, 16>), grid, dim3(HONU_BLOCK), 0, s, meta,
-                           var, acl, reg, payload_off, n, out, out_cap, out_off, status, acl_out);
-    else
-        hipLaunchKernelGGL((k_encode_meta_lane<true, 8>), grid, dim3(HONU_BLOCK), 0, s, meta,
-                           var, acl, reg, payload_off, n, out, out_cap, out_off, status, acl_out);
+    const bool line = (n + HONU_WAVE - 1) / HONU_WAVE > line_min_tiles;
+#define HONU_META_LANE(RG, U)                                                                        \
+    hipLaunchKernelGGL((k_encode_meta_lane<true, RG, U>), grid, dim3(HONU_BLOCK), 0, s, meta, var, acl, \
+                       reg, payload_off, n, out, out_cap, out_off, status, acl_out, payload)
+    if (line && payload) HONU_META_LANE(16, true);
+    else if (line) HONU_META_LANE(16, false);
+    else if (payload) HONU_META_LANE(8, true);
+    else HONU_META_LANE(8, false);
+#undef HONU_META_LANE
     return hipGetLastError();
 }
 

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define HONU_ABI_VERSION 4u  /* 4: ACL lists returned in place (HONU_ACL_INPLACE) */
+#define HONU_ABI_VERSION 5u  /* 5: honu_encode_*_units; 4: ACL lists returned in place (HONU_ACL_INPLACE) */
 #define HONU_STORAGE_VERSION 1u /* object.StorageVersion, object.go:14 */
 #define HONU_ULID_LEN 16
 #define HONU_KEY_LEN 29         /* keys.keySize, keys/keys.go:14 */
@@ -317,6 +317,23 @@ int32_t honu_encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint8_
 int32_t honu_encode_payloads(honu_ctx *ctx, const uint8_t *d_payload, const uint64_t *d_payload_off,
                              uint64_t n, uint8_t *d_out, uint64_t out_cap,
                              const uint64_t *d_out_off, const int32_t *d_status, void *stream);
+/* The same two phases split at the memory side's 64-byte write unit (ABI 5):
+ * honu_encode_records_units also writes each payload's bytes in the partial
+ * 64-byte units at its two ends (from d_payload), and honu_encode_payloads_units
+ * writes the whole units between, so no 64-byte unit of the records arena is
+ * written partly by both phases (a unit that leaves L2 partly written costs a
+ * read-modify-write: DESIGN §3 "the 64-byte write unit"; 1M Small step -1.6 %).
+ * Units are counted on absolute addresses of d_out. Records encoded by one of
+ * the pair are completed only by the other: never mix the two forms on a
+ * batch. honu_encode (one call) uses this form. */
+int32_t honu_encode_records_units(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,
+                                  const honu_acl *d_acl, const uint32_t *d_regions,
+                                  const uint8_t *d_payload, const uint64_t *d_payload_off, uint64_t n,
+                                  uint8_t *d_out, uint64_t out_cap, const uint64_t *d_out_off,
+                                  int32_t *d_status, void *stream);
+int32_t honu_encode_payloads_units(honu_ctx *ctx, const uint8_t *d_payload, const uint64_t *d_payload_off,
+                                   uint64_t n, uint8_t *d_out, uint64_t out_cap,
+                                   const uint64_t *d_out_off, const int32_t *d_status, void *stream);
 
 /* sizes + scan + encode in one call; d_out_off (n+1) is produced here. */
 int32_t honu_marshal_batch(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var,

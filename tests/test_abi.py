@@ -50,7 +50,7 @@ STRUCTS = ((META_DTYPE, "honu_meta"), (ACL_DTYPE, "honu_acl"), (INFO_DTYPE, "hon
 
 def test_abi_self_description():
     lib = _lib.load()
-    assert lib.honu_abi_version() == 4
+    assert lib.honu_abi_version() == 5
     assert lib.honu_sizeof_meta() == META_DTYPE.itemsize == 352
     assert lib.honu_sizeof_acl() == ACL_DTYPE.itemsize == 20
     assert lib.honu_sizeof_record_info() == INFO_DTYPE.itemsize == 32

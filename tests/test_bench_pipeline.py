@@ -236,6 +236,68 @@ def test_encode_payloads_respects_out_cap(oracle_lib):
     codec.close()
 
 
+@pytest.mark.parametrize("units", [1, 0], ids=["units_pair", "plain_pair"])
+@pytest.mark.parametrize("corpus", ["random", "small", "large"])
+def test_encode_pairs_bit_exact(oracle_lib, corpus, units):
+    """The two forms of the split encode, each phase on its own stream as the
+    bench runs them: honu_encode_records_units + honu_encode_payloads_units
+    (the encoder writes each payload's partial end 64-byte units, the copy the
+    whole ones; ABI 5) and honu_encode_records + honu_encode_payloads. Every
+    record's bytes equal oracle.marshal_batch's, with empty, tiny, unit-
+    aligned and unit-straddling payloads (random corpus: nil metas, empty
+    data, every frame size) and the output arena at several 64-byte phases."""
+    from corpora import random_metas
+    from honu_amd import object as hobj
+    from honu_amd.metadata import pack_batch
+    if corpus == "random":
+        metas, datas = random_metas(300, 91)
+        # payload lengths around the unit: 0..130 bytes, and a few long ones
+        datas = [None if d is None else bytes((j * 7 + k) & 0xFF for k in range((j * 37) % 131 if j % 5 else 4096 + j))
+                 for j, d in enumerate(datas)]
+        hb = pack_batch(metas, datas)
+    else:
+        hb = gen_host_batch(4, corpus, 0, 300 if corpus == "small" else 40)
+    n = len(hb.meta)
+    oout, ooff, ost = oracle_lib.marshal_batch(hb)
+    codec = hobj.Codec(0, 1024)
+    d = hobj.DeviceBatch.from_host(hb, codec.torch_device)
+    L = codec.lib
+    total = int(ooff[-1])
+    sizes = codec._empty(8 * (n + 1))
+    st = codec._empty(4 * n)
+    codec.encode_sizes(d, sizes, st)
+    codec.scan(sizes, n, sizes)
+    side = torch.cuda.Stream(codec.torch_device)
+    for phase in (0, 16, 48):  # the arena's start against the 64-byte units
+        buf = torch.full((total + 256,), 0xEE, dtype=torch.uint8, device=codec.torch_device)
+        out = buf[phase:]
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        side.wait_event(ev)
+        P = _lib.ptr
+        if units:
+            _lib.check(L.honu_encode_records_units(codec.ctx, P(d.meta), P(d.var), P(d.acl), P(d.regions),
+                                                   P(d.payload), P(d.payload_off), n, P(out), total,
+                                                   P(sizes), P(st), codec.stream), "records_units")
+            _lib.check(L.honu_encode_payloads_units(codec.ctx, P(d.payload), P(d.payload_off), n, P(out),
+                                                    total, P(sizes), P(st), side.cuda_stream), "payloads_units")
+        else:
+            _lib.check(L.honu_encode_records(codec.ctx, P(d.meta), P(d.var), P(d.acl), P(d.regions),
+                                             P(d.payload_off), n, P(out), total, P(sizes), P(st),
+                                             codec.stream), "records")
+            _lib.check(L.honu_encode_payloads(codec.ctx, P(d.payload), P(d.payload_off), n, P(out), total,
+                                              P(sizes), P(st), side.cuda_stream), "payloads")
+        torch.cuda.synchronize()
+        assert np.array_equal(_host(st, 4 * n, np.int32), ost)
+        assert np.array_equal(_host(sizes, 8 * (n + 1), np.uint64), ooff)
+        h = out.cpu().numpy()
+        for i in range(n):
+            if ost[i] == 0:
+                a, z = int(ooff[i]), int(ooff[i + 1])
+                assert h[a:z].tobytes() == oout[a:z].tobytes(), (phase, i)
+    codec.close()
+
+
 def test_bench_serial_verify(oracle_lib):
     """--serial (one stream, one output slot): each chunk is checked before
     the next one reuses the slot, and the bench's own verification passes."""
