@@ -265,7 +265,10 @@ HONU_DEV void k_encode_acl_grp_one(uint64_t i, const honu_meta *__restrict__ met
     const honu_acl *A = acl + ao;
     const uint64_t P = pos & ~ACL_ALL_PRESENT;
     if (pos & ACL_ALL_PRESENT) {  // whole chunks [ceil16(P), floor16(E))
-        const uint64_t X0 = (P + 15) & ~15ull, X1 = (P + 18 * na) & ~15ull;
+        // whole ACL_UNIT units on absolute addresses (lane.h writes the ends)
+        const uint64_t ab = (uint64_t)out;
+        const uint64_t X0 = ((ab + P + ACL_UNIT - 1) & ~(ACL_UNIT - 1)) - ab,
+                       X1 = ((ab + P + 18 * na) & ~(ACL_UNIT - 1)) - ab;
         if (X1 <= X0) return;
         const uint64_t nch = (X1 - X0) >> 4;
         constexpr int K = 2;  // chunks per lane computed before any store

@@ -476,6 +476,13 @@ HONU_DEV uint64_t encode_tail_bytes_noacl(const honu_meta &m, const uint32_t *__
     return t;
 }
 
+// The list kernel (k_encode_acl_grp) writes an all-present ACL list's whole
+// ACL_UNIT-byte units, this lane the list's bytes in the partial units at
+// its two ends (16: 16-byte chunks; 64: the memory side's write unit, so
+// that no unit is written by both kernels).
+#ifndef ACL_UNIT
+#define ACL_UNIT 16ull
+#endif
 // Header + Metadata tail of one record into out[beg, end) (the payload bytes
 // in between are the copy engine's). SKIP_ACL: leave the ACL entries to a
 // group writer: write the fields up to uvarint(len ACL), return that position
@@ -592,24 +599,40 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
             // list's bytes in the partial 16-byte chunks at both ends, so the
             // group kernel stores whole aligned chunks only
             acl_ret = P | ACL_ALL_PRESENT;
-            const uint64_t hend = ((P + 15) & ~15ull) < E ? ((P + 15) & ~15ull) : E;
-            const uint64_t T = (E & ~15ull) > hend ? (E & ~15ull) : hend;
-            // the list's encoding at both ends (acl_chunk: 16 bytes from the
-            // <= 2 entries they straddle), both loaded at once
-            const u32x4 hv = acl_chunk(acl + ao, na, P, P);
-            const u32x4 tv = E > T ? acl_chunk(acl + ao, na, P, T) : u32x4{0, 0, 0, 0};
-            auto put_n = [&](const u32x4 &v, uint32_t cnt) {  // the first cnt (< 16) bytes of v
+            // the list's bytes up to the first ACL_UNIT boundary and from the
+            // last one on (absolute addresses of out, as k_encode_acl_grp)
+            const uint64_t ab = (uint64_t)out;
+            const uint64_t hu = ((ab + P + ACL_UNIT - 1) & ~(ACL_UNIT - 1)) - ab;
+            const uint64_t hend = hu < E ? hu : E;
+            const uint64_t tu = ((ab + E) & ~(ACL_UNIT - 1)) - ab;
+            const uint64_t T = tu > hend ? tu : hend;
+            auto put_n = [&](const u32x4 &v, uint32_t cnt) {  // the first cnt (<= 16) bytes of v
                 const uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
                 if (cnt >= 8) {
                     W.put(lo, 8);
-                    if (cnt > 8) W.put(hi & ((1ull << (8 * (cnt - 8))) - 1), cnt - 8);
+                    if (cnt == 16) W.put(hi, 8);
+                    else if (cnt > 8) W.put(hi & ((1ull << (8 * (cnt - 8))) - 1), cnt - 8);
                 } else if (cnt) {
                     W.put(lo & ((1ull << (8 * cnt)) - 1), cnt);
                 }
             };
-            put_n(hv, (uint32_t)(hend - P));  // <= 43 + 15 since the drain
-            if (T > hend) W.jump(T);  // the whole chunks in between are k_encode_acl_grp's
-            put_n(tv, (uint32_t)(E - T));
+            // (acl_chunk: 16 bytes of the list's encoding from x, from the
+            // <= 2 entries they straddle)
+            if constexpr (ACL_UNIT == 16) {  // one piece of < 16 bytes at each end, both loaded at once
+                const u32x4 hv = acl_chunk(acl + ao, na, P, P);
+                const u32x4 tv = E > T ? acl_chunk(acl + ao, na, P, T) : u32x4{0, 0, 0, 0};
+                put_n(hv, (uint32_t)(hend - P));  // <= 43 + 15 since the drain
+                if (T > hend) W.jump(T);  // the whole chunks in between are k_encode_acl_grp's
+                put_n(tv, (uint32_t)(E - T));
+            } else {
+                W.drain();  // the ring holds < 16 chunks
+                for (uint64_t x = P; x < hend; x += 16)
+                    put_n(acl_chunk(acl + ao, na, P, x), (uint32_t)(hend - x < 16 ? hend - x : 16));
+                if (T > hend) W.jump(T);  // the whole units in between are k_encode_acl_grp's
+                for (uint64_t x = T; x < E; x += 16)
+                    put_n(acl_chunk(acl + ao, na, P, x), (uint32_t)(E - x < 16 ? E - x : 16));
+                W.drain();
+            }
         } else {
             acl_ret = P;
             W.jump(E);
