@@ -209,7 +209,8 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     // lb_resolve_grouped*)
     const uint64_t groups = (tiles / HONU_WAVE + 1) > LB_GROUPS ? tiles / HONU_WAVE + 1 : LB_GROUPS;
     const uint64_t lb_dec_words = 3 * tiles + 3 * groups;
-    const uint64_t lb_bytes = 2 * sizeof(LbState) + 8 * (lb_dec_words + scan_words);
+    // (+ the copies' range-tail counters: three 128-byte lines)
+    const uint64_t lb_bytes = 2 * sizeof(LbState) + 8 * (lb_dec_words + scan_words) + 3 * 4 * COPY_TICKET_STRIDE;
     const uint64_t bytes = 8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 32 * n +
                            8 * n + 4 * map_cap + lb_bytes + 256;
     if (hipMalloc(&c->ws, bytes) != hipSuccess) {
@@ -259,6 +260,8 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     c->lb_dec_gstatus = c->lb_dec_status + 3 * tiles;
     c->scan.status = c->lb_dec_status + c->lb_dec_words;
     c->scan.words = scan_words;
+    c->geom.copy_tickets = (uint32_t *)(c->scan.status + scan_words);
+    c->geom.copy_steal = 1;
     c->scan.max_blocks = 4 * prop.multiProcessorCount;
     c->lb_bytes = lb_bytes;
     // clean look-back state: epoch 0 with no published tile. On a stream of
@@ -308,6 +311,7 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
         __atomic_store_n(ctx->spec_seen, 0u, __ATOMIC_RELAXED);
         ctx->spec_off = (uint32_t)value;
     }
+    else if (!strcmp(name, "copy_steal") && (value == 0 || value == 1)) ctx->geom.copy_steal = (int)value;
     else if (!strcmp(name, "copy_variant") && value >= 0 && (value == 0 || HONU_AB_BUILD))
         ctx->geom.copy_variant = (int)value;
     else if (!strcmp(name, "encode_variant") && (value == 0 || (value == 1 && HONU_AB_BUILD)))
@@ -333,6 +337,7 @@ int32_t honu_ctx_get_param(const honu_ctx *ctx, const char *name, int64_t *value
         *value = __atomic_load_n(ctx->spec_seen + 1, __ATOMIC_RELAXED);
     else if (!strcmp(name, "speculate_backoff"))  // calls the next call starts without speculation
         *value = __atomic_load_n(ctx->spec_seen, __ATOMIC_RELAXED) ? SPEC_BACKOFF_CALLS : ctx->spec_off;
+    else if (!strcmp(name, "copy_steal")) *value = ctx->geom.copy_steal;
     else if (!strcmp(name, "copy_variant")) *value = ctx->geom.copy_variant;
     else if (!strcmp(name, "encode_variant")) *value = ctx->geom.encode_variant;
     else if (!strcmp(name, "record_variant")) *value = ctx->geom.record_variant;

@@ -142,31 +142,12 @@ HONU_DEV void copy_short_class(const Seg &seg, uint64_t n, uint64_t v, uint64_t 
     }
 }
 
-template <class Seg, int UNROLL, int NT, bool TWO = false>
-__global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t n,
-                                                               const uint64_t *__restrict__ total_p,
-                                                               uint64_t short_max = COPY_FEW_WAVES_MIN) {
-    uint64_t W = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
-    const uint64_t w = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + wave_in_block();
-    const uint64_t base = seg.lo();
-    const uint64_t total = *total_p - base;
-    // Large segments stream best from few waves (DRAM rows stay open: 2 WG per
-    // CU measured best); short segments are latency bound and want every wave
-    // the launch has (SMALL_SEG_WAVES_FACTOR x more).
-    const bool few = n && total / n >= COPY_FEW_WAVES_MIN;
-    if (few) {
-        const uint64_t Wall = W;
-        W /= SMALL_SEG_WAVES_FACTOR;
-        if constexpr (TWO) {
-            if (w >= W) {
-                copy_short_class<Seg, UNROLL>(seg, n, w - W, Wall - W, short_max);
-                return;
-            }
-        }
-    }
-    if (w >= W) return;
-    const uint64_t lo = base + ((total * w / W) & ~15ull);
-    const uint64_t hi = (w + 1 == W) ? base + total : base + ((total * (w + 1) / W) & ~15ull);
+// The logical range [lo, hi) of a streaming wave: its first segment by binary
+// search, then forward across segment boundaries (skip_short: segments under
+// short_max are the short class's).
+template <class Seg, int UNROLL, int NT>
+HONU_DEV void copy_range(const Seg &seg, uint64_t n, uint64_t lo, uint64_t hi, bool skip_short,
+                         uint64_t short_max) {
     if (lo >= hi) return;
     // largest i with start(i) <= lo
     uint64_t a = 0, b = n;  // invariant: start(a) <= lo, answer in [a, b)
@@ -196,13 +177,81 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t 
             ok_nx = seg.get(i + 1, len_nx, src_nx, dst_nx, skip_nx);
         }
         if (!ok) continue;
-        if (TWO && few && len < short_max) continue;  // the short class's
+        if (skip_short && len < short_max) continue;  // the short class's
         const uint64_t x = s > lo ? s : lo;
         const uint64_t e = s + len;
         const uint64_t y = e < hi ? e : hi;
         if (x < y)
             wave_copy<UNROLL, NT>(dst + (x - s), src + (x - s), y - x);
     }
+}
+
+// Range tails from a counter (tickets: the context's counter pair for this
+// kind of copy, nullptr: off). In a launch whose segments average at least
+// COPY_STEAL_MIN bytes, a streaming wave copies the first 1 - COPY_STEAL / 64
+// of its range, then takes the other streaming waves' range tails, in order,
+// from tickets[0]: the waves whose ranges hold fewer bytes to copy (a mixed
+// batch's short segments are skipped inside them) or that share their CU with
+// a metadata kernel take more tails instead of leaving the launch's end to
+// the slowest. tickets[1] counts the waves done, and the last one resets both,
+// so every launch finds them zero (as the look-back state; a replayed hipGraph
+// too). Measured (4 interleaved rounds each, profiles/r05/copy_steal/): 1M
+// Mixed encode -1.4 % per step (every copy launch -2 % in the kernel trace),
+// Mixed encode + decode -2.9 %, Medium -1.2 % (-3.5 % on another box), Large
+// equal; with it on 1M Small too, +1.9 % (2.6 KB payloads: hence the bound).
+#define COPY_STEAL_MIN (16u << 10)
+#define COPY_STEAL 8u
+template <class Seg, int UNROLL, int NT, bool TWO = false>
+__global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t n,
+                                                               const uint64_t *__restrict__ total_p,
+                                                               uint64_t short_max = COPY_FEW_WAVES_MIN,
+                                                               uint32_t *tickets = nullptr) {
+    uint64_t W = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
+    const uint64_t w = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + wave_in_block();
+    const uint64_t base = seg.lo();
+    const uint64_t total = *total_p - base;
+    // Large segments stream best from few waves (DRAM rows stay open: 2 WG per
+    // CU measured best); short segments are latency bound and want every wave
+    // the launch has (SMALL_SEG_WAVES_FACTOR x more).
+    const bool few = n && total / n >= COPY_FEW_WAVES_MIN;
+    if (few) {
+        const uint64_t Wall = W;
+        W /= SMALL_SEG_WAVES_FACTOR;
+        if constexpr (TWO) {
+            if (w >= W) {
+                copy_short_class<Seg, UNROLL>(seg, n, w - W, Wall - W, short_max);
+                return;
+            }
+        }
+    }
+    if (w >= W) return;
+    auto range = [&](uint64_t v, uint64_t &lo, uint64_t &hi) {
+        lo = base + ((total * v / W) & ~15ull);
+        hi = (v + 1 == W) ? base + total : base + ((total * (v + 1) / W) & ~15ull);
+    };
+    uint64_t lo, hi;
+    range(w, lo, hi);
+    if (tickets && n && total / n >= COPY_STEAL_MIN) {  // uniform over the launch
+        auto cut = [](uint64_t l, uint64_t h) {  // where a range's tail starts
+            return h - ((((h - l) * COPY_STEAL) >> 6) & ~15ull);
+        };
+        copy_range<Seg, UNROLL, NT>(seg, n, lo, cut(lo, hi), TWO && few, short_max);
+        for (;;) {
+            uint32_t t = 0;
+            if (__lane_id() == 0) t = atomicAdd(&tickets[0], 1u);
+            t = __shfl(t, 0);
+            if (t >= W) break;  // each wave's last take: W of them past the tails
+            uint64_t l, h;
+            range(t, l, h);
+            copy_range<Seg, UNROLL, NT>(seg, n, cut(l, h), h, TWO && few, short_max);
+        }
+        if (__lane_id() == 0 && atomicAdd(&tickets[1], 1u) == (uint32_t)W - 1) {
+            atomicExch(&tickets[0], 0u);  // every wave has taken its last ticket
+            atomicExch(&tickets[1], 0u);
+        }
+        return;
+    }
+    copy_range<Seg, UNROLL, NT>(seg, n, lo, hi, TWO && few, short_max);
 }
 
 #ifdef HONU_AB
@@ -272,11 +321,12 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_sweep(Seg seg, uint64_t n,
 // per-wave ranges {unroll, non-temporal}; 6-7 the sweep form; 11 / 12
 // non-temporal loads only / stores only; 13-15 one unaligned 16-byte load per
 // chunk instead of two aligned loads and a funnel; 40 without the short-
-// segment class. The product library has variant 0 only (unroll 4, default
+// segment class; 44 without the range tails (every variant but 0 runs
+// without them). The product library has variant 0 only (unroll 4, default
 // cache policy, two segment classes: measured fastest).
 template <class Seg>
 static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
-                              const uint64_t *total, hipStream_t s) {
+                              const uint64_t *total, uint32_t *tickets, hipStream_t s) {
     const dim3 grid(g.copy_blocks * SMALL_SEG_WAVES_FACTOR), block(HONU_BLOCK);
 #ifdef HONU_AB
     if (g.copy_variant >= 6 && g.copy_variant <= 7) {
@@ -301,6 +351,10 @@ static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
     case 14: hipLaunchKernelGGL((k_copy_segments<Seg, 8, 4>), grid, block, 0, s, seg, n, total); return hipGetLastError();
     case 15: hipLaunchKernelGGL((k_copy_segments<Seg, 2, 4>), grid, block, 0, s, seg, n, total); return hipGetLastError();
     case 40: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0, false>), grid, block, 0, s, seg, n, total); return hipGetLastError();
+    case 44:  // range tails off
+        hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0, true>), grid, block, 0, s, seg, n, total,
+                           (uint64_t)COPY_FEW_WAVES_MIN, nullptr);
+        return hipGetLastError();
     case 42: {  // the short class's bound from the environment (bytes)
         static const uint64_t sm = getenv("HONU_COPY_SHORT_MAX") ? strtoull(getenv("HONU_COPY_SHORT_MAX"), nullptr, 10)
                                                                  : (uint64_t)COPY_FEW_WAVES_MIN;
@@ -311,7 +365,7 @@ static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
     }
 #endif
     hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0, true>), grid, block, 0, s, seg, n, total,
-                       (uint64_t)COPY_FEW_WAVES_MIN);
+                       (uint64_t)COPY_FEW_WAVES_MIN, g.copy_steal ? tickets : nullptr);
     return hipGetLastError();
 }
 
@@ -321,7 +375,7 @@ hipError_t launch_encode_copy(const LaunchGeom &g, const uint8_t *payload,
                               bool units, hipStream_t s) {
     if (n == 0) return hipSuccess;
     EncodeSegments seg{payload, payload_off, out, out_cap, out_off, status, units};
-    return launch_copy(g, seg, n, payload_off + n, s);
+    return launch_copy(g, seg, n, payload_off + n, g.copy_tickets, s);
 }
 
 hipError_t launch_span_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t n,
@@ -329,7 +383,7 @@ hipError_t launch_span_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t n,
                             const uint64_t *offs, uint8_t *data, hipStream_t s) {
     if (n == 0) return hipSuccess;
     SpanSegments seg{rec, info, scratch, offs, data};
-    return launch_copy(g, seg, n, offs + n, s);
+    return launch_copy(g, seg, n, offs + n, g.copy_tickets + COPY_TICKET_STRIDE, s);
 }
 
 hipError_t launch_decode_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t n,
@@ -338,7 +392,7 @@ hipError_t launch_decode_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t 
                               hipStream_t s) {
     if (n == 0) return hipSuccess;
     DecodeSegments seg{rec, info, scratch, offs, data, n};
-    return launch_copy(g, seg, n, totals + 2, s);
+    return launch_copy(g, seg, n, totals + 2, g.copy_tickets + 2 * COPY_TICKET_STRIDE, s);
 }
 
 }  // namespace honu

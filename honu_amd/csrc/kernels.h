@@ -99,7 +99,10 @@ struct LaunchGeom {
                             // per-group / per-lane forms 1-4: DESIGN §3)
     uint32_t *tile_map;     // sweep-form tile -> segment map (context scratch)
     uint64_t tile_map_cap;
+    uint32_t *copy_tickets; // the copies' range-tail counters (copy.hip): encode, span, decode
+    int copy_steal;         // 1: range tails from the counters (default), 0: off
 };
+#define COPY_TICKET_STRIDE 32u  // uint32 words: one 128-byte line per kind of copy
 
 hipError_t launch_encode_copy(const LaunchGeom &g, const uint8_t *payload,
                               const uint64_t *payload_off, uint64_t n, uint8_t *out,

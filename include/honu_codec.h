@@ -196,8 +196,10 @@ typedef struct honu_ctx honu_ctx;
 /* Create a context on HIP device `device` with scratch for batches of up to
  * `max_records` records (scan partials, decode list positions). Allocation
  * happens here and only here. Returns NULL and sets *err on failure.
- * The scratch is per context: calls that use it (scan, decode) issued on
- * different streams concurrently need one context each. Arenas: the records
+ * The scratch is per context: calls that use it (scan, decode, and the payload
+ * copies of one kind — honu_encode_payloads*, honu_decode_payloads,
+ * honu_decode_data — with their range-tail counters, param "copy_steal")
+ * issued on different streams concurrently need one context each. Arenas: the records
  * arena, the materialised data arena and row arrays must be 16-byte aligned,
  * ACL and region tables 4-byte aligned (hipMalloc gives 256). */
 honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err);
@@ -219,7 +221,10 @@ int32_t honu_ctx_reset(honu_ctx *ctx, void *stream);
  * workgroups of the one-wave-per-record kernels, default 8 per CU),
  * "lane_blocks" (cap on workgroups of the lane, group and window kernels;
  * default 0 = no cap — a cap leaves room for a concurrent payload copy),
- * "copy_variant" (copy-engine variant, default 0), "record_variant" (how the
+ * "copy_variant" (copy-engine variant, default 0), "copy_steal" (1, the
+ * default: in a copy whose payloads average >= 16 KB each streaming wave
+ * copies 7/8 of its byte range, then the ranges' last eighths from a counter
+ * in the context; 0: fixed ranges only), "record_variant" (how the
  * per-record metadata kernels map records to lanes: 0 auto — the fastest
  * measured form per kernel, with honu_decode_batch running the single-launch
  * decode for batches of 48 K records or more; 5 the split decode at every

@@ -307,15 +307,21 @@ def test_long_tails_and_nil_entries_parity(codec, oracle_lib):
         assert unpack_row(meta[i], oout, acl, reg) == normalize(metas[i]), i
 
 
-@pytest.mark.parametrize("lens", ["tiny", "edges", "skew"])
-@pytest.mark.parametrize("copy_variant", [0, 1, 6, 11, 12, 13], ids=["default", "unroll8", "sweep", "nt_load", "nt_store", "unaligned"])
+@pytest.mark.parametrize("lens", ["tiny", "edges", "skew", "long", "mixed"])
+@pytest.mark.parametrize("copy_variant", [0, 1, 6, 11, 12, 13, 44],
+                         ids=["default", "unroll8", "sweep", "nt_load", "nt_store", "unaligned", "no_tails"])
 def test_copy_engine_parity(oracle_lib, copy_variant, lens):
     """The payload copy engine on awkward length mixes: payloads of 0-40 bytes
     (head/tail bytes only), lengths around multiples of 16, and a skewed mix of
     a few 300 KiB payloads among thousands of short ones (a wave range then
-    spans a long segment and many short ones). Both copy paths: the default
-    (short segments as 64-lane piece batches) and variant 8 (segment after
-    segment). Encoded bytes and materialised payloads are bit-exact."""
+    spans a long segment and many short ones), segments of 16-100 KB ("long":
+    the range tails taken from the counter) and a Mixed-like batch ("mixed":
+    average >= 64 KB, so the short-segment class and the range tails at
+    once). The default copy and, with the A/B build
+    (HONU_LIB_PATH=honu_amd/libhonu_codec_ab.so; skipped on the product
+    library), its measured variants: unroll 8, the sweep form, non-temporal
+    loads / stores, unaligned loads, no range tails (44). Encoded bytes and
+    materialised payloads are bit-exact."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     rng = np.random.default_rng(5)
@@ -324,6 +330,12 @@ def test_copy_engine_parity(oracle_lib, copy_variant, lens):
         ln = rng.integers(0, 41, n)
     elif lens == "edges":
         ln = (rng.integers(1, 200, n) * 16 + rng.integers(-2, 3, n)).clip(0)
+    elif lens == "long":
+        ln = rng.integers(16 << 10, 100 << 10, n)  # 58 KB on average
+    elif lens == "mixed":
+        ln = rng.integers(512, 4608, n)
+        big = rng.random(n) < 0.3
+        ln[big] = rng.integers(128 << 10, 400 << 10, int(big.sum()))  # 81 KB on average
     else:
         ln = rng.integers(0, 3000, n)
         ln[rng.integers(0, n, 12)] = 300 << 10
