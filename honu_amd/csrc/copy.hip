@@ -205,7 +205,8 @@ template <class Seg, int UNROLL, int NT, bool TWO = false>
 __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t n,
                                                                const uint64_t *__restrict__ total_p,
                                                                uint64_t short_max = COPY_FEW_WAVES_MIN,
-                                                               uint32_t *tickets = nullptr) {
+                                                               uint32_t *tickets = nullptr,
+                                                               uint32_t steal = COPY_STEAL) {
     uint64_t W = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
     const uint64_t w = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + wave_in_block();
     const uint64_t base = seg.lo();
@@ -232,8 +233,8 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t 
     uint64_t lo, hi;
     range(w, lo, hi);
     if (tickets && n && total / n >= COPY_STEAL_MIN) {  // uniform over the launch
-        auto cut = [](uint64_t l, uint64_t h) {  // where a range's tail starts
-            return h - ((((h - l) * COPY_STEAL) >> 6) & ~15ull);
+        auto cut = [&](uint64_t l, uint64_t h) {  // where a range's tail starts (steal / 64 of it)
+            return h - ((((h - l) * steal) >> 6) & ~15ull);
         };
         copy_range<Seg, UNROLL, NT>(seg, n, lo, cut(lo, hi), TWO && few, short_max);
         for (;;) {
@@ -321,8 +322,8 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_sweep(Seg seg, uint64_t n,
 // per-wave ranges {unroll, non-temporal}; 6-7 the sweep form; 11 / 12
 // non-temporal loads only / stores only; 13-15 one unaligned 16-byte load per
 // chunk instead of two aligned loads and a funnel; 40 without the short-
-// segment class; 44 without the range tails (every variant but 0 runs
-// without them). The product library has variant 0 only (unroll 4, default
+// segment class; 44 without the range tails (every variant but 0 and 45 runs
+// without them); 45 the tails' share from HONU_COPY_STEAL. The product library has variant 0 only (unroll 4, default
 // cache policy, two segment classes: measured fastest).
 template <class Seg>
 static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
@@ -351,6 +352,13 @@ static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
     case 14: hipLaunchKernelGGL((k_copy_segments<Seg, 8, 4>), grid, block, 0, s, seg, n, total); return hipGetLastError();
     case 15: hipLaunchKernelGGL((k_copy_segments<Seg, 2, 4>), grid, block, 0, s, seg, n, total); return hipGetLastError();
     case 40: hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0, false>), grid, block, 0, s, seg, n, total); return hipGetLastError();
+    case 45: {  // the range tails' share (/ 64) from the environment (HONU_COPY_STEAL)
+        static const uint32_t st = getenv("HONU_COPY_STEAL") ? (uint32_t)atoi(getenv("HONU_COPY_STEAL")) : COPY_STEAL;
+        if (st > 64) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0, true>), grid, block, 0, s, seg, n, total,
+                           (uint64_t)COPY_FEW_WAVES_MIN, tickets, st);
+        return hipGetLastError();
+    }
     case 44:  // range tails off
         hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0, true>), grid, block, 0, s, seg, n, total,
                            (uint64_t)COPY_FEW_WAVES_MIN, nullptr);
