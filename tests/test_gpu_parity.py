@@ -7,6 +7,8 @@ decoder error vectors and on a fuzzed corpus of malformed records. Full-size
 batches are checked through size-independent properties (payload digests
 survive encode -> decode; a sample of records equals the oracle's bytes).
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -308,8 +310,9 @@ def test_long_tails_and_nil_entries_parity(codec, oracle_lib):
 
 
 @pytest.mark.parametrize("lens", ["tiny", "edges", "skew", "long", "mixed"])
-@pytest.mark.parametrize("copy_variant", [0, 1, 6, 11, 12, 13, 44],
-                         ids=["default", "unroll8", "sweep", "nt_load", "nt_store", "unaligned", "no_tails"])
+@pytest.mark.parametrize("copy_variant", [0, -1, 1, 6, 11, 12, 13, 44],
+                         ids=["default", "steal_off", "unroll8", "sweep", "nt_load", "nt_store", "unaligned",
+                              "no_tails"])
 def test_copy_engine_parity(oracle_lib, copy_variant, lens):
     """The payload copy engine on awkward length mixes: payloads of 0-40 bytes
     (head/tail bytes only), lengths around multiples of 16, and a skewed mix of
@@ -320,7 +323,8 @@ def test_copy_engine_parity(oracle_lib, copy_variant, lens):
     once). The default copy and, with the A/B build
     (HONU_LIB_PATH=honu_amd/libhonu_codec_ab.so; skipped on the product
     library), its measured variants: unroll 8, the sweep form, non-temporal
-    loads / stores, unaligned loads, no range tails (44). Encoded bytes and
+    loads / stores, unaligned loads, no range tails (44); "steal_off": the
+    product copy with the context param copy_steal 0. Encoded bytes and
     materialised payloads are bit-exact."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -347,7 +351,15 @@ def test_copy_engine_parity(oracle_lib, copy_variant, lens):
     hb = HostBatch(base.meta, base.var, base.acl, base.regions, pay, off)
     c = hobj.Codec(0, n)
     try:
-        if c.lib.honu_ctx_set_param(c.ctx, b"copy_variant", copy_variant) != 0:
+        if copy_variant < 0:  # the range tails off (honu_codec.h "copy_steal")
+            v = ctypes.c_int64(-1)
+            hobj._lib.check(c.lib.honu_ctx_get_param(c.ctx, b"copy_steal", ctypes.byref(v)), "param")
+            assert v.value == 1  # the default
+            assert c.lib.honu_ctx_set_param(c.ctx, b"copy_steal", 2) != 0
+            hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"copy_steal", 0), "param")
+            hobj._lib.check(c.lib.honu_ctx_get_param(c.ctx, b"copy_steal", ctypes.byref(v)), "param")
+            assert v.value == 0
+        elif c.lib.honu_ctx_set_param(c.ctx, b"copy_variant", copy_variant) != 0:
             pytest.skip("A/B copy variant: not in the product library")
         out, goff, st = gpu_marshal(c, hb)
         oout, ooff, ost = oracle_lib.marshal_batch(hb)
