@@ -126,8 +126,7 @@ struct SpanSegments {
 // (Every wave on every segment instead: Mixed 7 % slower, the long segments'
 // streams too many.)
 template <class Seg, int UNROLL>
-HONU_DEV void copy_short_class(const Seg &seg, uint64_t n, uint64_t v, uint64_t V, uint64_t short_max) {
-    const uint64_t i0 = n * v / V, i1 = n * (v + 1) / V;
+HONU_DEV void copy_short_run(const Seg &seg, uint64_t i0, uint64_t i1, uint64_t short_max) {
     uint64_t len_nx = 0, skip = 0;
     const uint8_t *src_nx = nullptr;
     uint8_t *dst_nx = nullptr;
@@ -139,6 +138,34 @@ HONU_DEV void copy_short_class(const Seg &seg, uint64_t n, uint64_t v, uint64_t 
         const bool ok = ok_nx;
         if (i + 1 < i1) ok_nx = seg.get(i + 1, len_nx, src_nx, dst_nx, skip);
         if (ok && len < short_max) wave_copy<UNROLL, 0>(dst, src, len);
+    }
+}
+
+// tickets (A/B build, variant 46): the index runs' last eighths from a
+// counter pair, as the long class's range tails (below)
+template <class Seg, int UNROLL, bool TAILS = false>
+HONU_DEV void copy_short_class(const Seg &seg, uint64_t n, uint64_t v, uint64_t V, uint64_t short_max,
+                               uint32_t *tickets = nullptr) {
+    if constexpr (!TAILS) {
+        copy_short_run<Seg, UNROLL>(seg, n * v / V, n * (v + 1) / V, short_max);
+        (void)tickets;
+        return;
+    }
+    auto cut = [&](uint64_t u) {  // where run u's tail starts
+        const uint64_t a = n * u / V, b = n * (u + 1) / V;
+        return b - (((b - a) * 8) >> 6);
+    };
+    copy_short_run<Seg, UNROLL>(seg, n * v / V, cut(v), short_max);
+    for (;;) {
+        uint32_t t = 0;
+        if (__lane_id() == 0) t = atomicAdd(&tickets[0], 1u);
+        t = __shfl(t, 0);
+        if (t >= V) break;
+        copy_short_run<Seg, UNROLL>(seg, cut(t), n * (t + 1) / V, short_max);
+    }
+    if (__lane_id() == 0 && atomicAdd(&tickets[1], 1u) == (uint32_t)V - 1) {
+        atomicExch(&tickets[0], 0u);
+        atomicExch(&tickets[1], 0u);
     }
 }
 
@@ -201,12 +228,13 @@ HONU_DEV void copy_range(const Seg &seg, uint64_t n, uint64_t lo, uint64_t hi, b
 // equal; with it on 1M Small too, +1.9 % (2.6 KB payloads: hence the bound).
 #define COPY_STEAL_MIN (16u << 10)
 #define COPY_STEAL 8u
-template <class Seg, int UNROLL, int NT, bool TWO = false>
+template <class Seg, int UNROLL, int NT, bool TWO = false, bool STAILS = false>
 __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t n,
                                                                const uint64_t *__restrict__ total_p,
                                                                uint64_t short_max = COPY_FEW_WAVES_MIN,
                                                                uint32_t *tickets = nullptr,
-                                                               uint32_t steal = COPY_STEAL) {
+                                                               uint32_t steal = COPY_STEAL,
+                                                               uint32_t *short_tickets = nullptr) {
     uint64_t W = (uint64_t)gridDim.x * HONU_WAVES_PER_BLOCK;
     const uint64_t w = (uint64_t)blockIdx.x * HONU_WAVES_PER_BLOCK + wave_in_block();
     const uint64_t base = seg.lo();
@@ -220,7 +248,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_segments(Seg seg, uint64_t 
         W /= SMALL_SEG_WAVES_FACTOR;
         if constexpr (TWO) {
             if (w >= W) {
-                copy_short_class<Seg, UNROLL>(seg, n, w - W, Wall - W, short_max);
+                copy_short_class<Seg, UNROLL, STAILS>(seg, n, w - W, Wall - W, short_max, short_tickets);
                 return;
             }
         }
@@ -323,7 +351,8 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_copy_sweep(Seg seg, uint64_t n,
 // non-temporal loads only / stores only; 13-15 one unaligned 16-byte load per
 // chunk instead of two aligned loads and a funnel; 40 without the short-
 // segment class; 44 without the range tails (every variant but 0 and 45 runs
-// without them); 45 the tails' share from HONU_COPY_STEAL. The product library has variant 0 only (unroll 4, default
+// without them); 45 the tails' share from HONU_COPY_STEAL; 46 the range tails
+// and the short class's run tails. The product library has variant 0 only (unroll 4, default
 // cache policy, two segment classes: measured fastest).
 template <class Seg>
 static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
@@ -359,6 +388,10 @@ static hipError_t launch_copy(const LaunchGeom &g, const Seg &seg, uint64_t n,
                            (uint64_t)COPY_FEW_WAVES_MIN, tickets, st);
         return hipGetLastError();
     }
+    case 46:  // + the short class's run tails (tickets[2..3] of the kind's line)
+        hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0, true, true>), grid, block, 0, s, seg, n, total,
+                           (uint64_t)COPY_FEW_WAVES_MIN, tickets, COPY_STEAL, tickets + 2);
+        return hipGetLastError();
     case 44:  // range tails off
         hipLaunchKernelGGL((k_copy_segments<Seg, 4, 0, true>), grid, block, 0, s, seg, n, total,
                            (uint64_t)COPY_FEW_WAVES_MIN, nullptr);

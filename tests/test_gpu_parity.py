@@ -310,9 +310,9 @@ def test_long_tails_and_nil_entries_parity(codec, oracle_lib):
 
 
 @pytest.mark.parametrize("lens", ["tiny", "edges", "skew", "long", "mixed"])
-@pytest.mark.parametrize("copy_variant", [0, -1, 1, 6, 11, 12, 13, 44],
+@pytest.mark.parametrize("copy_variant", [0, -1, 1, 6, 11, 12, 13, 44, 46],
                          ids=["default", "steal_off", "unroll8", "sweep", "nt_load", "nt_store", "unaligned",
-                              "no_tails"])
+                              "no_tails", "short_tails"])
 def test_copy_engine_parity(oracle_lib, copy_variant, lens):
     """The payload copy engine on awkward length mixes: payloads of 0-40 bytes
     (head/tail bytes only), lengths around multiples of 16, and a skewed mix of
@@ -323,7 +323,8 @@ def test_copy_engine_parity(oracle_lib, copy_variant, lens):
     once). The default copy and, with the A/B build
     (HONU_LIB_PATH=honu_amd/libhonu_codec_ab.so; skipped on the product
     library), its measured variants: unroll 8, the sweep form, non-temporal
-    loads / stores, unaligned loads, no range tails (44); "steal_off": the
+    loads / stores, unaligned loads, no range tails (44), the short class's
+    run tails too (46); "steal_off": the
     product copy with the context param copy_steal 0. Encoded bytes and
     materialised payloads are bit-exact."""
     if not torch.cuda.is_available():
