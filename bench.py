@@ -229,6 +229,7 @@ class Bench:
         self.data_cap = max(int(alloc[a:b].sum()) for a, b in self.chunks) + 16
         self.out_cap = max(self.rec_bytes) + 16
         self.ncu = torch.cuda.get_device_properties(self.dev).multi_processor_count
+        self._copy_form = {}
         if not pipeline:
             return
         nslots = 1 if args.serial else max(2, getattr(args, "slots", 2))
@@ -259,6 +260,11 @@ class Bench:
                                                            args.meta_blocks * ncu), "param")
                 _lib.check(self.lib.honu_ctx_set_param(sl.codec.ctx, b"lane_blocks",
                                                        self.lane_blocks * ncu), "param")
+        var, steal = ctypes.c_int64(0), ctypes.c_int64(0)
+        c0 = self.slots[0].codec.ctx
+        _lib.check(self.lib.honu_ctx_get_param(c0, b"copy_variant", ctypes.byref(var)), "param")
+        _lib.check(self.lib.honu_ctx_get_param(c0, b"copy_steal", ctypes.byref(steal)), "param")
+        self._copy_form = {"copy_variant": var.value, "copy_range_tails": bool(steal.value)}
         self.sm = torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio < 0 else 0)  # metadata kernels
         # payload copies: the bandwidth-bound critical path, dispatched first
         self.sc = (torch.cuda.Stream(self.dev, priority=-1 if args.copy_prio > 0 else 0)
@@ -494,6 +500,12 @@ class Bench:
     # chunks (box-dependent, -2 % to +4 % for the single launch) and keep the
     # encode copy faster (5.84 vs 5.63-5.67 TB/s, profiles/r02/crossover_static_tiles.txt)
     FUSED_DECODE_MIN = 128 << 10
+
+    def copy_form(self):
+        """The payload copy's form on the output slots' contexts, read when
+        they were set up: the copy variant (0 in the product library) and
+        whether the range tails (honu_codec.h "copy_steal") are on."""
+        return self._copy_form
 
     def recoveries(self):
         """Recovery launches the output slots' single-launch decodes have run
@@ -1503,6 +1515,7 @@ def pipeline_leg(args, shape, encode_only, rank, local, world, dist, barrier, ga
         },
         "encode_copy_gbs": enc_gbs,
         "metadata_decode": None if encode_only else ("fused" if bench.fused_decode(bench.C) else "split"),
+        **bench.copy_form(),
         "decode_recoveries_in_timed_steps": None if encode_only else recoveries,
         "verified": verified,
         "verified_scope": None if verified is None else Bench.VERIFIED_SCOPE + (
@@ -1682,6 +1695,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
             "metadata_streams": len(bench.sms),
             "copy_streams": 1 if bench.sd is bench.sc else 2,
             "metadata_decode": "fused" if bench.fused_decode(bench.C) else "split",
+            **bench.copy_form(),
             "decode_recoveries_in_timed_steps": recoveries,
         },
         "records_per_s": total_records / step_s,
