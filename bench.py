@@ -110,8 +110,10 @@ def parse_args(argv=None):
                         "per-record output-offset prefix scan, headers + tails, payload copy)")
     p.add_argument("--legs", default="auto",
                    help="encdec mode, comma list of extra legs after the main one: small (1M Small "
-                        "encode + decode, configs[1]), mixed_encode (1M Mixed encode, configs[3]); "
-                        "auto: both for the default Large line, none otherwise; none: no legs")
+                        "encode + decode, configs[1]), mixed_encode (1M Mixed encode, configs[3]), "
+                        "medium (1M Medium encode + decode), xlarge (--records/16 XLarge encode + "
+                        "decode + chunk zero copy); auto: all four for the default Large line, none "
+                        "otherwise; none: no legs")
     p.add_argument("--decode-prio", type=int, default=0, choices=[0, 1],
                    help="1: a chunk's single-launch decode (and its guarded launch) on a high-priority "
                         "stream of its slot, so the guard's workgroups are dispatched before the other "
@@ -726,13 +728,14 @@ class DecodeBench:
         self.acl_cap, self.reg_cap = self.nacl + 1, self.nreg + 1
         self.dacl, self.dreg = E(20 * self.acl_cap), E(4 * self.reg_cap)
         self.totals = E(32)
-        # ACL table entries the default (in-place) form writes: the lists with
-        # a nil entry only (none in the generator's records), from one
-        # untimed decode
+        # table entries the default (in-place) forms write: ACL lists with a
+        # nil entry only (none in the generator's records), no regions; from
+        # one untimed decode
         self._zero_copy_once(s)
         st.synchronize()
-        self.acl_table_entries = int(self.totals[:8].view(torch.int64).item())
-        self.meta_bytes = self.meta_bytes_for(self.acl_table_entries)
+        tt = self.totals[:16].view(torch.int64).tolist()
+        self.acl_table_entries, self.reg_table_entries = int(tt[0]), int(tt[1])
+        self.meta_bytes = self.meta_bytes_for(self.acl_table_entries, self.reg_table_entries)
         # materialising leg: two data slots of one chunk each
         self.slots = []
         for _ in range(2):
@@ -747,15 +750,15 @@ class DecodeBench:
         self.sv = torch.cuda.Stream(dev)
         torch.cuda.synchronize()
 
-    def meta_bytes_for(self, acl_table_entries):
+    def meta_bytes_for(self, acl_table_entries, reg_table_entries):
         """Algorithmic bytes of one Metadata() + zero-copy Data() pass (SURVEY
         §8d): per record the offsets pair, the header and the Metadata tail
-        read; the row, the record info, 4 per region and 20 per ACL TABLE
-        entry written (a list returned in place writes nothing: its entries
-        are read as part of the tail)."""
+        read; the row, the record info, 4 per region TABLE entry and 20 per
+        ACL TABLE entry written (a list returned in place writes nothing: its
+        entries are read as part of the tail)."""
         N = self.b.N
         return (8 * N + self.hdr_bytes + self.tail_bytes + 352 * N + 32 * N +
-                20 * acl_table_entries + 4 * self.nreg)
+                20 * acl_table_entries + 4 * reg_table_entries)
 
     # -- zero copy, whole batch ------------------------------------------------
     def _zero_copy_once(self, s):
@@ -778,35 +781,55 @@ class DecodeBench:
         torch.cuda.synchronize()
         return [x.elapsed_time(y) for x, y in ev]
 
-    def zero_copy(self, reps):
-        """The default decode (ACL lists returned in place, HONU_ACL_INPLACE),
-        then the same call with every list copied into the ACL table (context
-        param acl_inplace 0, the form of rounds 1-4) for comparison."""
+    def _form_reps(self, acl, reg, reps):
+        """reps timed calls with the context params acl_inplace / regions_inplace
+        set to (acl, reg): (per-call ms, ACL table entries, region table entries)."""
         c = self.codec.ctx
-        _lib.check(self.lib.honu_ctx_set_param(c, b"acl_inplace", 0), "param")
-        ms_tab = self._zero_copy_reps(reps)
-        tab_entries = int(self.totals[:8].view(torch.int64).item())
-        _lib.check(self.lib.honu_ctx_set_param(c, b"acl_inplace", 1), "param")
+        _lib.check(self.lib.honu_ctx_set_param(c, b"acl_inplace", acl), "param")
+        _lib.check(self.lib.honu_ctx_set_param(c, b"regions_inplace", reg), "param")
         ms = self._zero_copy_reps(reps)
+        tt = self.totals[:16].view(torch.int64).tolist()
+        return ms, int(tt[0]), int(tt[1])
+
+    def _form_summary(self, ms, acl_entries, reg_entries, how):
         t = sum(ms) / len(ms) / 1e3
-        t_tab = sum(ms_tab) / len(ms_tab) / 1e3
+        nb = self.meta_bytes_for(acl_entries, reg_entries)
+        return {"ms": t * 1e3, "ms_min": min(ms), "records_per_s": self.b.N / t,
+                "acl_table_entries": acl_entries, "region_table_entries": reg_entries,
+                "algorithmic_bytes_per_launch": nb, "frac_of_spec": nb / t / 1e9 / HBM_PEAK_GBS,
+                "how": how}
+
+    def zero_copy(self, reps):
+        """The default decode (ACL and region lists returned in place,
+        HONU_ACL_INPLACE / HONU_REGIONS_INPLACE), then, for comparison, the
+        same call with every list in its table (context params acl_inplace 0,
+        regions_inplace 0: rounds 1-4) and with the ACL lists in place but the
+        regions in their table (round 5's default). The forms alternate, the
+        default's reps split around the others."""
+        h = max(1, reps // 2)
+        ms = self._form_reps(1, 1, h)[0]
+        ms_tab, tab_acl, tab_reg = self._form_reps(0, 0, reps)
+        ms_r5, r5_acl, r5_reg = self._form_reps(1, 0, reps)
+        ms2, acl_e, reg_e = self._form_reps(1, 1, reps - h)
+        ms = ms + ms2
+        t = sum(ms) / len(ms) / 1e3
         N = self.b.N
         gbs = self.meta_bytes / t / 1e9
-        tab_bytes = self.meta_bytes_for(tab_entries)
         return {
             "records": N,
             "reps": reps,
             "ms": t * 1e3,
             "ms_min": min(ms),
             "records_per_s": N / t,
-            "acl_form": (f"in place (HONU_ACL_INPLACE): lists with every entry present stay in the "
-                         f"records arena; {self.acl_table_entries} ACL table entries written"),
-            "acl_table_form": {"ms": t_tab * 1e3, "ms_min": min(ms_tab), "records_per_s": N / t_tab,
-                               "acl_table_entries": tab_entries,
-                               "algorithmic_bytes_per_launch": tab_bytes,
-                               "frac_of_spec": tab_bytes / t_tab / 1e9 / HBM_PEAK_GBS,
-                               "how": "the same call with acl_inplace 0: every list copied into "
-                                      "the 20-byte ACL table (rounds 1-4)"},
+            "list_forms": (f"in place (HONU_ACL_INPLACE, HONU_REGIONS_INPLACE): ACL lists with every "
+                           f"entry present and every region list stay in the records arena; "
+                           f"{acl_e} ACL and {reg_e} region table entries written"),
+            "table_form": self._form_summary(
+                ms_tab, tab_acl, tab_reg, "the same call with acl_inplace 0 and regions_inplace 0: "
+                "every list copied into the 20-byte ACL and 4-byte region tables (rounds 1-4)"),
+            "regions_table_form": self._form_summary(
+                ms_r5, r5_acl, r5_reg, "the same call with regions_inplace 0: ACL lists in place, "
+                "region lists in their table (round 5's default)"),
             "calls": "honu_decode_batch(data arena NULL) over all records, one call",
             "roofline": {
                 "bound": "hbm",
@@ -820,11 +843,12 @@ class DecodeBench:
                 "traffic": (pmc_traffic(self.workload("zero_copy"), "k_decode_fused<1, 0, true>")
                             or pmc_traffic(self.workload("zero_copy"), "k_decode_fused<1, 1, true>")
                             or pmc_traffic(self.workload("zero_copy"), "k_decode_fused<0, 0, true>")),
+                "traffic_commit": pmc_commit(self.workload("zero_copy")),
                 "avg_launch_ms": t * 1e3,
                 "algorithmic_bytes_per_launch": self.meta_bytes,
                 "algorithmic_bytes": "8 (offsets) + header + Metadata tail read; 352 row + 32 info "
-                                     "+ 4 per region + 20 per ACL TABLE entry written, per record "
-                                     "(in-place lists: none)",
+                                     "+ 4 per region TABLE entry + 20 per ACL TABLE entry written, "
+                                     "per record (in-place lists: none)",
             },
         }
 
@@ -958,6 +982,7 @@ class DecodeBench:
                 "frac": cg / HBM_PEAK_GBS,
                 "traffic": pmc_traffic(self.workload("materialising"),
                                        "k_copy_segments<honu::DecodeSegments"),
+                "traffic_commit": pmc_commit(self.workload("materialising")),
                 "launches": len(copy_ms),
                 "avg_launch_ms": sum(copy_ms) / len(copy_ms),
                 "algorithmic_bytes_per_launch": sum(copy_bytes) / len(copy_bytes),
@@ -1013,17 +1038,27 @@ class DecodeBench:
 FUSED_DECODE_MIN = 48 << 10
 
 
+def _pmc_entry(workload):
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(tpath):
+        return {}
+    return json.load(open(tpath)).get("workloads", {}).get(workload, {})
+
+
 def pmc_traffic(workload, kernel_prefix):
     """HBM bytes per launch of kernel from the PMC passes of this same command
     (profiles/pmc_traffic.json, tools/pmc_traffic.py), or None."""
-    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(tpath):
-        return None
-    pm = json.load(open(tpath)).get("workloads", {}).get(workload, {})
+    pm = _pmc_entry(workload)
     for k, v in pm.get("kernels", {}).items():
         if k.startswith("void honu::" + kernel_prefix) or k.startswith("honu::" + kernel_prefix):
             return v["traffic_per_launch"]
     return None
+
+
+def pmc_commit(workload):
+    """The commit the PMC passes of the workload's entry were measured on
+    (tools/pmc_traffic.py records it), or None."""
+    return _pmc_entry(workload).get("commit")
 
 
 def hbm_probe(codec, dev, nbytes=4 << 30, reps=5):
@@ -1413,13 +1448,18 @@ def decode_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
     }
 
 
-LEG_SHAPES = {"small": ("small", False), "mixed_encode": ("mixed", True)}
+# leg -> (shape, encode only, records per GPU as a fraction of --records,
+# the chunk zero-copy decode too)
+LEG_SHAPES = {"small": ("small", False, 1, False), "mixed_encode": ("mixed", True, 1, False),
+              "medium": ("medium", False, 1, False), "xlarge": ("xlarge", False, 1 / 16, True)}
 
 
 def legs_of(args):
     """The extra legs of an encdec line (--legs): configs[1] (1M Small encode
-    + decode) and configs[3] (1M Mixed encode) ride along with the default
-    1M Large line, so that the driver's own run measures them too."""
+    + decode), configs[3] (1M Mixed encode) and the README's other two shapes
+    north_star names (1M Medium encode + decode; 64 K XLarge encode + decode,
+    i.e. --records / 16, with its chunk zero-copy decode) ride along with the
+    default 1M Large line, so that the driver's own run measures every shape."""
     if args.legs == "none":
         return []
     if args.legs == "auto":
@@ -1432,16 +1472,22 @@ def legs_of(args):
     return legs
 
 
-def pipeline_leg(args, shape, encode_only, rank, local, world, dist, barrier, gather_max, all_ok):
+def pipeline_leg(args, shape, encode_only, rank, local, world, dist, barrier, gather_max, all_ok,
+                 records=None, zero_copy=False):
     """One timed pipelined configuration of this rank's --records records of
     `shape` (a Bench of its own, released at the end): warmup, barrier, the
     timed steps, barrier; max over ranks. encode_only: object.Marshal only
     (configs[3]: size pass, output-offset prefix scan, headers + tails,
     payload copy), else encode + materialising decode (configs[1]). Returns
     the leg's dict (value in GiB/s of records over all ranks, the dominant
-    copy kernel's roofline, the whole step's algorithmic HBM fraction)."""
+    copy kernel's roofline, the whole step's algorithmic HBM fraction).
+    records: records per GPU (default --records); zero_copy: also the
+    Metadata() + zero-copy Data() decode of the leg's largest chunk, alone
+    (Bench.zero_copy_decode), after the check."""
     la = argparse.Namespace(**vars(args))
     la.shape = shape
+    if records:
+        la.records = int(records)
     bench = Bench(la, rank, local, encode_only=encode_only)
     for _ in range(la.warmup):
         bench.step()
@@ -1471,6 +1517,7 @@ def pipeline_leg(args, shape, encode_only, rank, local, world, dist, barrier, ga
     other_ms = [x[4].elapsed_time(x[5]) for x in bench.events]  # decode copy / offsets
     enc_gbs = sum(pay) / (sum(enc_ms) / 1e3) / 1e9
     verified = None if la.no_verify else bench.verify()
+    zc = bench.zero_copy_decode() if zero_copy and not encode_only else None
     bench.release()
     verified = all_ok(verified)
     what = "encode (object.Marshal)" if encode_only else \
@@ -1509,6 +1556,7 @@ def pipeline_leg(args, shape, encode_only, rank, local, world, dist, barrier, ga
             "unit": "GB/s",
             "frac": kgbs / HBM_PEAK_GBS,
             "traffic": pmc_traffic(workload, kern.split(">")[0]),
+            "traffic_commit": pmc_commit(workload),
             "launches": len(kms),
             "avg_launch_ms": sum(kms) / max(1, len(kms)),
             "algorithmic_bytes_per_launch": sum(pay) / max(1, len(pay)),
@@ -1521,6 +1569,12 @@ def pipeline_leg(args, shape, encode_only, rank, local, world, dist, barrier, ga
         "verified_scope": None if verified is None else Bench.VERIFIED_SCOPE + (
             " (the records decoded untimed, zero copy, for the check)" if encode_only else ""),
     }
+    if zc is not None:
+        out["zero_copy_decode"] = {
+            "records": zc["records"], "ms": zc["ms"], "records_per_s": zc["records_per_s"],
+            "cold_ms": zc["cold_ms"], "cold_records_per_s": zc["cold_records_per_s"],
+            "how": "honu_decode_batch (data arena NULL) of the leg's largest chunk, alone, 10 reps "
+                   "warm and 10 after a 1 GiB scrub each (cold)"}
     if encode_only:  # configs[3] names the per-record output-offset prefix scan
         out["offsets_ms_per_step"] = sum(other_ms) / la.steps
         out["offsets"] = ("size pass (k_encode_sizes_grp) + exclusive scan (k_scan_lb) of every "
@@ -1533,11 +1587,11 @@ def pipeline_leg(args, shape, encode_only, rank, local, world, dist, barrier, ga
 def run_legs(args, rank, local, world, dist, barrier, gather_max, all_ok):
     legs = {}
     for name in legs_of(args):
-        shape, enc = LEG_SHAPES[name]
+        shape, enc, frac, zc = LEG_SHAPES[name]
         gc.collect()
         torch.cuda.empty_cache()
         legs[name] = pipeline_leg(args, shape, enc, rank, local, world, dist, barrier, gather_max,
-                                  all_ok)
+                                  all_ok, records=max(1, int(args.records * frac)), zero_copy=zc)
     return legs or None
 
 
@@ -1715,6 +1769,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
             "frac_of_achievable": dom_gbs / probe["copy_gbs"],
             "traffic": traffic,
             "traffic_source": "profiles/pmc_traffic.json" if traffic else None,
+            "traffic_commit": pmc_commit(workload),
             "launches": launches,
             "avg_launch_ms": dom_ms / launches,
             "algorithmic_bytes_per_launch": sum(enc_bytes) / launches,

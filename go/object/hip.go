@@ -27,6 +27,7 @@ package object
 import "C"
 
 import (
+	"encoding/binary"
 	"errors"
 	"fmt"
 	"io"
@@ -282,13 +283,18 @@ func flatten(metas []*metadata.Metadata, datas [][]byte) *batch {
 		r.permissions = C.uint8_t(m.Permissions)
 		if len(m.ACL) > 0 {
 			r.acl_off, r.acl_count = C.uint64_t(a), C.uint64_t(len(m.ACL))
+			nb := uint64(0) // the list's encoded length, carried (HONU_ACL_SIZED): the size pass reads no entry
 			for _, e := range m.ACL {
 				acls[a] = C.honu_acl{}
-				if e != nil { // a nil entry encodes as one 0x00 flag byte
+				nb++ // a nil entry encodes as one 0x00 flag byte
+				if e != nil {
 					acls[a].client_id, acls[a].permissions, acls[a].present = cULID(e.ClientID), C.uint8_t(e.Permissions), 1
+					nb += 17 // 01 | ClientID | Permissions (acls.go:26-39)
 				}
 				a++
 			}
+			r.acl_bytes = C.uint64_t(nb)
+			pr |= C.HONU_ACL_SIZED
 		}
 		if len(m.WriteRegions) > 0 {
 			r.regions_off, r.regions_count = C.uint64_t(g), C.uint64_t(len(m.WriteRegions))
@@ -422,7 +428,9 @@ func (c *Codec) DecodeBatch(objs []Object) ([]*metadata.Metadata, [][]byte, []er
 	//    needs more, the call's d_totals says exactly how many (records past a
 	//    cap get HONU_ERR_CAPACITY and nothing else changes): re-allocate to the
 	//    totals and decode again. An ACL list whose entries are all present
-	//    comes back in place (HONU_ACL_INPLACE) and takes no table entry.
+	//    comes back in place (HONU_ACL_INPLACE) and takes no table entry, and
+	//    so does every region list (HONU_REGIONS_INPLACE): with the defaults
+	//    only lists holding a nil ACL entry need the tables.
 	//    honu_amd/c_abi_demo.c runs this flow in C.
 	rows, info := device(uintptr(n)*uintptr(C.sizeof_honu_meta)), device(uintptr(n)*uintptr(C.sizeof_honu_record_info))
 	tot, hTot := device(32), pinned(32)
@@ -507,7 +515,8 @@ func (c *Codec) DecodeBatch(objs []Object) ([]*metadata.Metadata, [][]byte, []er
 // (region.go:160), time 0 is time.Time{} (decode.go:224-237). An ACL list
 // returned in place (HONU_ACL_INPLACE) is read from the arena: entry k is the
 // 18 bytes 01 | ClientID | Permissions at acl_off + 18 k (acls.go:26-51);
-// otherwise from the ACL table, where present == 0 is a nil entry.
+// otherwise from the ACL table, where present == 0 is a nil entry. A region
+// list returned in place (HONU_REGIONS_INPLACE) is read from the arena too.
 func unflatten(r *C.honu_meta, arena []byte, acl []C.honu_acl, regs []uint32) *metadata.Metadata {
 	frame := func(s C.honu_span) []byte {
 		if s.len == 0 {
@@ -571,8 +580,20 @@ func unflatten(r *C.honu_meta, arena []byte, acl []C.honu_acl, regs []uint32) *m
 			}
 		}
 	}
-	for k := range m.WriteRegions {
-		m.WriteRegions[k] = region.Region(regs[uint64(r.regions_off)+uint64(k)])
+	if p&C.HONU_REGIONS_INPLACE != 0 {
+		// in place: the list's uvarints in the arena, read as Regions.Decode
+		// reads them (region.go:154-169 -> lani DecodeUint32: at most 5 bytes,
+		// truncated to uint32, decode.go:127-146); the GPU decode validated them
+		q := uint64(r.regions_off)
+		for k := range m.WriteRegions {
+			v, w := binary.Uvarint(arena[q:min(q+5, uint64(len(arena)))])
+			m.WriteRegions[k] = region.Region(uint32(v))
+			q += uint64(w)
+		}
+	} else {
+		for k := range m.WriteRegions {
+			m.WriteRegions[k] = region.Region(regs[uint64(r.regions_off)+uint64(k)])
+		}
 	}
 	if p&C.HONU_HAS_PUBLISHER != 0 {
 		m.Publisher = &metadata.Publisher{PublisherID: ulidOf(r.publisher_id), ClientID: ulidOf(r.client_id),

@@ -76,6 +76,27 @@ static void acl_entry(const honu_meta *m, const uint8_t *rec, const honu_acl *ta
     *perm = a->permissions;
 }
 
+/* The regions of a decoded row, as the binding's Regions.Decode loop builds
+ * them (region.go:154-169): in place (HONU_REGIONS_INPLACE), the uvarints
+ * from regions_off of the records arena, each read as lani.DecodeUint32 does
+ * (<= 5 bytes, truncated to uint32; the GPU decode validated them); otherwise
+ * row j of the list in the region table. */
+static void region_values(const honu_meta *m, const uint8_t *rec, const uint32_t *table, uint32_t *out) {
+    if (!(m->present & HONU_REGIONS_INPLACE)) {
+        memcpy(out, table + m->regions_off, 4 * m->regions_count);
+        return;
+    }
+    const uint8_t *p = rec + m->regions_off;
+    for (uint64_t j = 0; j < m->regions_count; j++) {
+        uint64_t v = 0;
+        for (int k = 0, sh = 0; k < 5; k++, sh += 7) {
+            v |= (uint64_t)(p[0] & 0x7F) << sh;
+            if (!(*p++ & 0x80)) break;
+        }
+        out[j] = (uint32_t)v;
+    }
+}
+
 static void *h2d(const void *h, uint64_t bytes) {
     void *d = honu_device_alloc(bytes + 16);
     if (d && bytes && honu_memcpy_h2d(d, h, bytes, NULL) != HONU_OK) return NULL;
@@ -85,13 +106,20 @@ static void *h2d(const void *h, uint64_t bytes) {
 int main(int argc, char **argv) {
     const int32_t shape = argc > 1 ? atoi(argv[1]) : HONU_SHAPE_SMALL;
     const uint64_t n = argc > 2 ? strtoull(argv[2], NULL, 10) : 4096;
-    const char *dump_dir = argc > 3 ? argv[3] : NULL;
+    const char *dump_dir = argc > 3 && strcmp(argv[3], "-") ? argv[3] : NULL;
+    /* "table": every ACL and region list in its table (context params
+     * acl_inplace 0, regions_inplace 0); default: the library's in-place forms */
+    const int table_form = argc > 4 && !strcmp(argv[4], "table");
     const uint64_t seed = 12345;
     int32_t err = 0;
     honu_ctx *ctx = honu_ctx_create(0, n, &err);
     if (!ctx) {
         fprintf(stderr, "honu_ctx_create: %s (%s)\n", honu_status_string(err), honu_last_error());
         return 2;
+    }
+    if (table_form) {
+        CHECK(honu_ctx_set_param(ctx, "acl_inplace", 0));
+        CHECK(honu_ctx_set_param(ctx, "regions_inplace", 0));
     }
     /* 1. the host batch, as the Go side's flatten() would build it */
     uint64_t tot[4];
@@ -134,17 +162,19 @@ int main(int argc, char **argv) {
     const uint64_t rec_bytes = off[n];
     /* 4. Metadata() + zero-copy Data(), then a materialising decode. The ACL
      * and region tables are sized by the batch's entry counts: a first call
-     * with small caps (one entry per record here, so the retry always runs;
-     * a binding would start from its typical counts) reports the totals in
-     * d_totals (records past the caps get HONU_ERR_CAPACITY), the tables are
-     * re-allocated to exactly the totals and the call is repeated. Sizing them
-     * by record bytes instead (an entry takes >= 1 byte) would allocate
-     * 20 + 4 bytes per RECORD BYTE: 24x the records arena. */
+     * with small caps (a binding starts from its typical counts: none with
+     * the in-place forms, whose tables take only ACL lists with a nil entry;
+     * one entry per record with the table forms, so the retry always runs
+     * there) reports the totals in d_totals (records past the caps get
+     * HONU_ERR_CAPACITY), the tables are re-allocated to exactly the totals
+     * and the call is repeated. Sizing them by record bytes instead (an entry
+     * takes >= 1 byte) would allocate 20 + 4 bytes per RECORD BYTE: 24x the
+     * records arena. */
     honu_meta *d_meta = (honu_meta *)honu_device_alloc(sizeof(honu_meta) * n);
     honu_record_info *d_info = (honu_record_info *)honu_device_alloc(sizeof(honu_record_info) * n);
     uint64_t *d_tot = (uint64_t *)honu_device_alloc(32);
     NEED(d_meta && d_info && d_tot);
-    uint64_t acl_cap = n, reg_cap = n, totals[4] = {0, 0, 0, 0};
+    uint64_t acl_cap = table_form ? n : 0, reg_cap = table_form ? n : 0, totals[4] = {0, 0, 0, 0};
     honu_acl *d_tacl = NULL;
     uint32_t *d_treg = NULL;
     int calls = 0;
@@ -196,7 +226,9 @@ int main(int argc, char **argv) {
             return 1;
         }
     }
-    uint64_t lists_inplace = 0, lists_table = 0;
+    uint64_t lists_inplace = 0, lists_table = 0, regions_inplace = 0;
+    uint32_t *rv = (uint32_t *)honu_host_alloc(4 * 4096);
+    NEED(rv);
     for (uint64_t i = 0; i < n; i++) {
         const honu_meta *a = rows + i, *b = meta + i;
         if (info[i].meta_status != HONU_OK || info[i].data_status != HONU_OK ||
@@ -219,6 +251,13 @@ int main(int argc, char **argv) {
             }
         }
         if (b->acl_count) (b->present & HONU_ACL_INPLACE) ? lists_inplace++ : lists_table++;
+        if (b->regions_count > 4096) return 1;  /* (the generator writes at most 9) */
+        region_values(b, rec, treg, rv);
+        if (memcmp(rv, reg + a->regions_off, 4 * a->regions_count) != 0) {
+            fprintf(stderr, "record %llu: regions differ\n", (unsigned long long)i);
+            return 1;
+        }
+        if (b->regions_count && (b->present & HONU_REGIONS_INPLACE)) regions_inplace++;
     }
     CHECK(honu_decode_batch(ctx, d_out, d_off, n, d_meta, d_info, d_tacl, acl_cap, d_treg,
                             reg_cap, d_data, data_cap, d_tot, NULL));
@@ -237,10 +276,11 @@ int main(int argc, char **argv) {
     }
     printf("ok: %llu records, %llu encoded bytes, marshal + decode + materialise through the C ABI; "
            "decode calls %d, table bytes %llu (ACL entries %llu, regions %llu); ACL lists in place "
-           "%llu, in the table %llu\n",
+           "%llu, in the table %llu; region lists in place %llu\n",
            (unsigned long long)n, (unsigned long long)rec_bytes, calls, (unsigned long long)table_bytes,
            (unsigned long long)totals[0], (unsigned long long)totals[1],
-           (unsigned long long)lists_inplace, (unsigned long long)lists_table);
+           (unsigned long long)lists_inplace, (unsigned long long)lists_table,
+           (unsigned long long)regions_inplace);
     honu_ctx_destroy(ctx);
     return 0;
 }

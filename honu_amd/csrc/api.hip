@@ -45,10 +45,24 @@ struct honu_ctx {
     hipEvent_t ev_fork, ev_join;
     int enc_fork;            // honu_ctx_set_param("encode_fork", 0 off / 1 on / 2 auto: when lane_blocks caps the grid)
     bool acl_inplace;        // honu_ctx_set_param("acl_inplace"): decode returns all-present ACL lists in place
+    bool reg_inplace;        // honu_ctx_set_param("regions_inplace"): decode returns region lists in place
     bool inline_recovery;    // honu_ctx_set_param("inline_recovery"): ticket-form launches recover in-launch
     int guard_blocks;        // honu_ctx_set_param("guard_blocks"): one-wave workgroups of the guarded launch
                              // (0: as many as the speculative launch has waves)
+    uint32_t copy_seq;       // copy calls issued: call k takes counter line k % COPY_TICKET_LINES
+    int enc_form;            // the last honu_encode_records* call: 0 none, 1 plain, 2 units
 };
+
+// The launch geometry of one payload-copy call: the context's, with the
+// range-tail counters of the next line of the ring (kernels.h), so copy calls
+// in flight at once on different streams each count on a line of their own
+// (one shared line let a launch skip tails another one took).
+static LaunchGeom copy_geom(honu_ctx *ctx) {
+    LaunchGeom g = ctx->geom;
+    const uint32_t k = __atomic_fetch_add(&ctx->copy_seq, 1u, __ATOMIC_RELAXED) % COPY_TICKET_LINES;
+    g.copy_tickets = ctx->geom.copy_tickets + (uint64_t)k * COPY_TICKET_STRIDE;
+    return g;
+}
 static constexpr uint32_t SPEC_BACKOFF_CALLS = 16;
 
 static thread_local char g_last_error[256];
@@ -106,9 +120,18 @@ static bool stream_is_restricted(hipStream_t s, int num_cu) {
     return any && !all;
 }
 
+// The product library takes its configuration from honu_ctx_set_param only:
+// it behaves the same whatever the caller's process environment holds. The
+// A/B build (make ab) also reads HONU_* variables at context creation, for
+// tools/*.sh sweeps that cannot set params.
 static int env_int(const char *name, int dflt) {
+#ifdef HONU_AB
     const char *v = getenv(name);
     return v && *v ? atoi(v) : dflt;
+#else
+    (void)name;
+    return dflt;
+#endif
 }
 
 extern "C" {
@@ -194,6 +217,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     if (c->geom.record_variant != 5 && c->geom.record_variant != 6)
         c->geom.record_variant = 0;
     c->acl_inplace = env_int("HONU_ACL_INPLACE", 1) != 0;
+    c->reg_inplace = env_int("HONU_REGIONS_INPLACE", 1) != 0;
     // measured slower than the guarded launch (1M Small zero copy 0.56 ->
     // 0.67-0.70 ms, the Small step 4.17-4.21 -> 4.26-4.42 ms; DESIGN §3
     // "Round 5"): off by default
@@ -209,8 +233,9 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     // lb_resolve_grouped*)
     const uint64_t groups = (tiles / HONU_WAVE + 1) > LB_GROUPS ? tiles / HONU_WAVE + 1 : LB_GROUPS;
     const uint64_t lb_dec_words = 3 * tiles + 3 * groups;
-    // (+ the copies' range-tail counters: three 128-byte lines)
-    const uint64_t lb_bytes = 2 * sizeof(LbState) + 8 * (lb_dec_words + scan_words) + 3 * 4 * COPY_TICKET_STRIDE;
+    // (+ the copies' range-tail counters: a ring of 128-byte lines)
+    const uint64_t lb_bytes =
+        2 * sizeof(LbState) + 8 * (lb_dec_words + scan_words) + COPY_TICKET_LINES * 4 * COPY_TICKET_STRIDE;
     const uint64_t bytes = 8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 32 * n +
                            8 * n + 4 * map_cap + lb_bytes + 256;
     if (hipMalloc(&c->ws, bytes) != hipSuccess) {
@@ -305,6 +330,7 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
     else if (!strcmp(name, "speculate") && (value == 0 || value == 1)) ctx->spec_allowed = value != 0;
     else if (!strcmp(name, "encode_fork") && value >= 0 && value <= 2) ctx->enc_fork = (int)value;
     else if (!strcmp(name, "acl_inplace") && (value == 0 || value == 1)) ctx->acl_inplace = value != 0;
+    else if (!strcmp(name, "regions_inplace") && (value == 0 || value == 1)) ctx->reg_inplace = value != 0;
     else if (!strcmp(name, "inline_recovery") && (value == 0 || value == 1)) ctx->inline_recovery = value != 0;
     else if (!strcmp(name, "guard_blocks") && value >= 0 && value <= 65536) ctx->guard_blocks = (int)value;
     else if (!strcmp(name, "speculate_backoff") && value >= 0 && value <= (int64_t)SPEC_BACKOFF_CALLS) {
@@ -331,6 +357,7 @@ int32_t honu_ctx_get_param(const honu_ctx *ctx, const char *name, int64_t *value
     else if (!strcmp(name, "speculate")) *value = ctx->spec_allowed ? 1 : 0;
     else if (!strcmp(name, "encode_fork")) *value = ctx->enc_fork;
     else if (!strcmp(name, "acl_inplace")) *value = ctx->acl_inplace ? 1 : 0;
+    else if (!strcmp(name, "regions_inplace")) *value = ctx->reg_inplace ? 1 : 0;
     else if (!strcmp(name, "inline_recovery")) *value = ctx->inline_recovery ? 1 : 0;
     else if (!strcmp(name, "guard_blocks")) *value = ctx->guard_blocks;
     else if (!strcmp(name, "recoveries"))  // recovery launches that ran, since the context was created
@@ -383,6 +410,7 @@ static int32_t encode_records(honu_ctx *ctx, const honu_meta *d_meta, const uint
     if (!aligned(d_acl, 4) || !aligned(d_regions, 4)) return arg_fail("tables must be 4-byte aligned");
     HIPCHK(hipSetDevice(ctx->device));
     if (n > ctx->max_n) return HONU_E_WORKSPACE;
+    ctx->enc_form = units ? 2 : 1;  // (the payload call checks it: never mix the two forms)
 #ifdef HONU_AB
     if (ctx->geom.encode_variant == 1 && !units) {  // one launch, 16 lanes per record (enc.hip, A/B build only)
         HIPCHK(launch_encode_tail_grp(d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
@@ -447,8 +475,14 @@ static int32_t encode_payloads(honu_ctx *ctx, const uint8_t *d_payload, const ui
                                const int32_t *d_status, bool units, void *stream) {
     if (!ctx) return arg_fail("ctx");
     if (n && (!d_payload_off || !d_out || !d_out_off || !d_status)) return arg_fail("null pointer");
+    // the units pair completes only what its own records call left out: a
+    // payload call of the other form than the context's last records call
+    // would leave bytes unwritten (or write them twice) with every status OK
+    if (ctx->enc_form && ctx->enc_form != (units ? 2 : 1))
+        return arg_fail(units ? "honu_encode_payloads_units after honu_encode_records (mixed forms)"
+                              : "honu_encode_payloads after honu_encode_records_units (mixed forms)");
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(launch_encode_copy(ctx->geom, d_payload, d_payload_off, n, d_out, out_cap, d_out_off,
+    HIPCHK(launch_encode_copy(copy_geom(ctx), d_payload, d_payload_off, n, d_out, out_cap, d_out_off,
                               d_status, units, (hipStream_t)stream));
     return HONU_OK;
 }
@@ -473,6 +507,14 @@ int32_t honu_encode(honu_ctx *ctx, const honu_meta *d_meta, const uint8_t *d_var
     (void)var_len;
     (void)acl_len;
     (void)regions_len;
+    if (!d_payload) {  // a batch of empty payloads only (nothing to copy): the plain pair,
+                       // which reads the arena only for a non-empty payload
+        int32_t st = honu_encode_records(ctx, d_meta, d_var, d_acl, d_regions, d_payload_off, n, d_out,
+                                         out_cap, d_out_off, d_status, stream);
+        if (st) return st;
+        return honu_encode_payloads(ctx, d_payload, d_payload_off, n, d_out, out_cap, d_out_off, d_status,
+                                    stream);
+    }
     // the payload-unit pair (one kernel per 64-byte unit of the output)
     int32_t st = honu_encode_records_units(ctx, d_meta, d_var, d_acl, d_regions, d_payload, d_payload_off, n,
                                            d_out, out_cap, d_out_off, d_status, stream);
@@ -509,7 +551,7 @@ int32_t honu_decode_parse(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(launch_decode_parse_win(d_rec, d_rec_off, n, d_meta, d_info, ctx->scratch,
                                    ctx->reg_inline, ctx->counts, ctx->geom.lane_blocks,
-                                   ctx->acl_inplace, (hipStream_t)stream));
+                                   ctx->acl_inplace, ctx->reg_inplace, (hipStream_t)stream));
     return HONU_OK;
 }
 
@@ -541,7 +583,7 @@ int32_t honu_decode_payloads(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n,
     if (!d_data || !aligned(d_data, 16)) return arg_fail("data arena");
     HIPCHK(hipSetDevice(ctx->device));
     const uint64_t *tot = d_totals ? d_totals : ctx->totals;
-    HIPCHK(launch_decode_copy(ctx->geom, d_rec, n, d_info, ctx->scratch, ctx->offs, tot, d_data,
+    HIPCHK(launch_decode_copy(copy_geom(ctx), d_rec, n, d_info, ctx->scratch, ctx->offs, tot, d_data,
                               (hipStream_t)stream));
     return HONU_OK;
 }
@@ -590,7 +632,7 @@ int32_t honu_decode_records(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t 
                                regions_cap, materialize != 0, data_cap, ctx->scratch, ctx->offs,
                                tot, ctx->lb_dec, ctx->lb_dec_status, ctx->lb_dec_gstatus,
                                ctx->lb_dec_words, fused_blocks(ctx->geom), ctx->spec_seen,
-                               ctx->spec_seen + 1, spec, ctx->acl_inplace, ctx->inline_recovery,
+                               ctx->spec_seen + 1, spec, ctx->acl_inplace, ctx->reg_inplace, ctx->inline_recovery,
                                ctx->guard_blocks, s));
     return HONU_OK;
 }
@@ -659,7 +701,7 @@ int32_t honu_decode_data_copy(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n,
     if (n && (!d_rec || !d_info || !d_data)) return arg_fail("null pointer");
     if (!aligned(d_data, 16)) return arg_fail("data arena must be 16-byte aligned");
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(launch_span_copy(ctx->geom, d_rec, n, d_info, ctx->scratch, ctx->offs, d_data,
+    HIPCHK(launch_span_copy(copy_geom(ctx), d_rec, n, d_info, ctx->scratch, ctx->offs, d_data,
                             (hipStream_t)stream));
     return HONU_OK;
 }

@@ -213,8 +213,10 @@ HONU_DEV void copy_range(const Seg &seg, uint64_t n, uint64_t lo, uint64_t hi, b
     }
 }
 
-// Range tails from a counter (tickets: the context's counter pair for this
-// kind of copy, nullptr: off). In a launch whose segments average at least
+// Range tails from a counter (tickets: this launch's counter pair, one line of
+// a ring of COPY_TICKET_LINES lines in the context that successive copy calls
+// take in turn, so copies running at once on different streams never share
+// one: ADVICE r05; nullptr: off). In a launch whose segments average at least
 // COPY_STEAL_MIN bytes, a streaming wave copies the first 1 - COPY_STEAL / 64
 // of its range, then takes the other streaming waves' range tails, in order,
 // from tickets[0]: the waves whose ranges hold fewer bytes to copy (a mixed
@@ -418,13 +420,14 @@ hipError_t launch_encode_copy(const LaunchGeom &g, const uint8_t *payload,
     EncodeSegments seg{payload, payload_off, out, out_cap, out_off, status, units};
     return launch_copy(g, seg, n, payload_off + n, g.copy_tickets, s);
 }
+// (g.copy_tickets: the launch's own counter line, api.hip copy_geom)
 
 hipError_t launch_span_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t n,
                             const honu_record_info *info, const DecodeScratch *scratch,
                             const uint64_t *offs, uint8_t *data, hipStream_t s) {
     if (n == 0) return hipSuccess;
     SpanSegments seg{rec, info, scratch, offs, data};
-    return launch_copy(g, seg, n, offs + n, g.copy_tickets + COPY_TICKET_STRIDE, s);
+    return launch_copy(g, seg, n, offs + n, g.copy_tickets, s);
 }
 
 hipError_t launch_decode_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t n,
@@ -433,7 +436,7 @@ hipError_t launch_decode_copy(const LaunchGeom &g, const uint8_t *rec, uint64_t 
                               hipStream_t s) {
     if (n == 0) return hipSuccess;
     DecodeSegments seg{rec, info, scratch, offs, data, n};
-    return launch_copy(g, seg, n, totals + 2, g.copy_tickets + 2 * COPY_TICKET_STRIDE, s);
+    return launch_copy(g, seg, n, totals + 2, g.copy_tickets, s);
 }
 
 }  // namespace honu

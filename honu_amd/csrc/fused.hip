@@ -34,6 +34,7 @@ struct DecodeOut {
     DecodeScratch *scratch;   // materialize: payload sources for honu_decode_payloads
     uint64_t *offs;           // materialize: offs[3i+2] = data arena offset
     uint64_t *totals;         // column totals (3)
+    bool reg_inplace;         // region lists returned in place (HONU_REGIONS_INPLACE)
 };
 
 // Launches of at least this many tiles speculate (publish + ACL flags, below)
@@ -331,6 +332,16 @@ struct SpecPub {
 // not resident yet, so a launch-wide wait could deadlock beside another
 // persistent kernel.
 //
+// The recovery count (a measurement, honu_ctx_get_param "recoveries") in the
+// context's pinned word: one thread of one wave updates it per recovery, so a
+// plain load and store, no read-modify-write atomic over PCIe (which needs
+// platform atomics support: ADVICE r05).
+HONU_DEV void count_recovery(uint32_t *recoveries) {
+    if (!recoveries) return;
+    const uint32_t v = __hip_atomic_load(recoveries, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(recoveries, v + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // WPB: waves per workgroup (4; the guarded launch, k_decode_guard below: 1).
 template <int MODE, int FORM, bool INPL, int WPB>
 HONU_DEV void decode_fused_body(
@@ -344,8 +355,7 @@ HONU_DEV void decode_fused_body(
     // then decodes the context's next calls without speculation (api.hip)
     if (mode == 2 && spec_seen && blockIdx.x == 0 && threadIdx.x == 0) {
         __hip_atomic_store(spec_seen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        // (a count apart from the back-off flag, for measurements)
-        if (recoveries) __hip_atomic_fetch_add(recoveries, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        count_recovery(recoveries);  // (a count apart from the back-off flag, for measurements)
     }
     constexpr bool STAT = FORM != FORM_TICKET;
     constexpr uint32_t WAVE_BYTES = form_wave_bytes<FORM>();
@@ -406,7 +416,7 @@ HONU_DEV void decode_fused_body(
         // the recovery pass tells the host (once: the wave holding its first tile)
         if (pass == 1 && t == 0 && spec_seen && lane == 0) {
             __hip_atomic_store(spec_seen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (recoveries) __hip_atomic_fetch_add(recoveries, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            count_recovery(recoveries);
         }
         const uint64_t i0 = t * HONU_WAVE, i = i0 + lane;
         const uint64_t lim = i0 + HONU_WAVE < n ? i0 + HONU_WAVE : n;  // the tile's records are [i0, lim)
@@ -422,7 +432,7 @@ HONU_DEV void decode_fused_body(
         early.status = lb_status;
         early.t = t;
         early.ep = tag;
-        win_walk(i0, ws, rec, lim, H, R, P, early, INPL);
+        win_walk(i0, ws, rec, lim, H, R, P, early, INPL, O.reg_inplace);
 
         // counts -> offsets: wave scan + look-back across tiles
         uint64_t agg[3], excl[3], x0, x1, x2;
@@ -475,11 +485,19 @@ HONU_DEV void decode_fused_body(
             WSTAMP(14);
         }
 #endif
+        // zero copy: a tile with no table entry (ACL and region lists in
+        // place) uses none of its prefixes, so it does not wait for its
+        // predecessors (the launch's last tile does, for the totals). A
+        // materialising decode waits in every tile: each record's data-arena
+        // offset (offs[3i+2], also for an empty payload) is the copy's sorted
+        // segment start (copy.hip DecodeSegments).
+        const bool need = t == ntiles - 1 || agg[0] || agg[1] || O.materialize;
         if constexpr (STAT)  // every tile runs at once: grouped prefixes (lookback.h)
-            lb_resolve_grouped<3>(lb_status, lb_gstatus, t, ntiles, tag, agg, excl);
+            lb_resolve_grouped<3>(lb_status, lb_gstatus, t, ntiles, tag, agg, excl, need);
         else  // tickets: a decoupled look-back over the group totals (the plain
               // one over tile words, lb_resolve, measured 3 % slower on 1M Small)
-            lb_resolve_grouped_lb<3>(lb_status, lb_gstatus, t, ntiles, tag, agg, excl);
+            lb_resolve_grouped_lb<3>(lb_status, lb_gstatus, t, ntiles, tag, agg, excl, need);
+        if (!need) excl[0] = excl[1] = excl[2] = 0;  // (offsets of zero entries: unused)
         WSTAMP(11);  // look-back wait
         // nothing is staged in the in-place form: the next ticket is requested
         // here, and the rest of the tile hides its round trip
@@ -668,8 +686,8 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
                                uint64_t data_cap, DecodeScratch *scratch, uint64_t *offs,
                                uint64_t *totals, LbState *lb, uint64_t *lb_status,
                                uint64_t *lb_gstatus, uint64_t lb_words, int max_blocks, uint32_t *spec_seen,
-                               uint32_t *recoveries, bool allow_spec, bool inplace, bool inline_rec,
-                               int guard_blocks, hipStream_t s) {
+                               uint32_t *recoveries, bool allow_spec, bool inplace, bool reg_inplace,
+                               bool inline_rec, int guard_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
     // (32-record tiles for batches whose 64-record tiles fill at most half the
     // resident waves, so that every SIMD walks records, measured slower with
@@ -679,7 +697,7 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
     const uint64_t tiles = (n + HONU_WAVE - 1) / HONU_WAVE;
     uint64_t b = (tiles + HONU_WAVES_PER_BLOCK - 1) / HONU_WAVES_PER_BLOCK;
     if (max_blocks > 0 && b > (uint64_t)max_blocks) b = (uint64_t)max_blocks;
-    DecodeOut O{meta, info, acl, acl_cap, reg, reg_cap, data_cap, materialize, scratch, offs, totals};
+    DecodeOut O{meta, info, acl, acl_cap, reg, reg_cap, data_cap, materialize, scratch, offs, totals, reg_inplace};
     // speculation pays where tiles queue for tickets (1M Small 0.866 -> 0.840
     // ms with the publish alone, -> 0.778 with the ACL flags too) and, since
     // the flag gather is gone, in static-tile launches of ~1000 tiles and more

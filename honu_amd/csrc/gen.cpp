@@ -54,12 +54,17 @@ const uint64_t kVarHeader = 64;  // (the shared strings take 50 bytes; 16-aligne
 // var arena, as a binding's flatten may lay them out, so the tail encoder's
 // aligned 16-byte frame loads do not straddle a block they do not need
 // (VERDICT r04 item 4). The encoded records are the same either way.
+// (A/B build only: the product library reads no environment variable.)
 bool var_align() {
+#ifdef HONU_AB
     static const int v = [] {
         const char *e = getenv("HONU_GEN_VAR_ALIGN");
         return e && *e ? atoi(e) : 0;
     }();
     return v != 0;
+#else
+    return false;
+#endif
 }
 
 struct Rng {
@@ -156,6 +161,10 @@ void gen_one(uint64_t seed, int shape, uint64_t index, Sink &s, honu_meta *row) 
         const uint64_t na = r.intn(64) + 1;
         m.acl_off = s.acl_n;
         m.acl_count = na;
+        // the list's encoded length, as a binding's flatten carries it while it
+        // copies m.ACL (HONU_ACL_SIZED: every entry present, 18 bytes each)
+        m.acl_bytes = 18 * na;
+        m.present |= HONU_ACL_SIZED;
         for (uint64_t i = 0; i < na; i++) {
             honu_acl a;
             memset(&a, 0, sizeof a);

@@ -54,7 +54,11 @@ HONU_DEV void k_encode_sizes_grp_one(uint64_t i, uint8_t *smem, const honu_meta 
         const uint64_t ao = m.acl_off, ro = m.regions_off;
         if (na) ok = ok && ao <= acl_len && na <= acl_len - ao;
         if (nr) ok = ok && ro <= reg_len && nr <= reg_len - ro;
-        ok = ok && !(pr & HONU_ACL_INPLACE);  // a decode output row: its list is not in the table
+        ok = ok && !(pr & (HONU_ACL_INPLACE | HONU_REGIONS_INPLACE));  // a decode output row: lists not in the tables
+        // a carried list length (HONU_ACL_SIZED): 1..18 bytes per entry (the
+        // list kernel checks it exactly against the entries)
+        const bool sized = (pr & HONU_ACL_SIZED) != 0;
+        if (sized) ok = ok && m.acl_bytes >= na && m.acl_bytes <= 18 * na;
         if (!ok) {
             stc = HONU_ERR_INPUT;
         } else {
@@ -71,7 +75,9 @@ HONU_DEV void k_encode_sizes_grp_one(uint64_t i, uint8_t *smem, const honu_meta 
             t += gframe_len(m.mime.len) + 33;  // MIME, Owner, Group, Permissions
             t += uvarint_len(na) + uvarint_len(nr);
             uint64_t part = 0;  // this lane's share of the lists
-            for (uint64_t k = r; k < na; k += G) part += acl[ao + k].present ? 18 : 1;
+            if (sized) t += m.acl_bytes;  // no ACL entry read
+            else
+                for (uint64_t k = r; k < na; k += G) part += acl[ao + k].present ? 18 : 1;
             for (uint64_t k = r; k < nr; k += G) part += uvarint_len(reg[ro + k]);
             t += 3;  // Publisher, Encryption, Compression flags
             if (pr & HONU_HAS_PUBLISHER) t += 32 + gframe_len(m.ip_address.len) + gframe_len(m.user_agent.len);
@@ -231,7 +237,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_grp(
 // every entry is present (the lane encoder's own test, lane.h).
 template <int G, bool SELF>
 HONU_DEV void k_encode_acl_grp_one(uint64_t i, const honu_meta *__restrict__ meta, const honu_acl *__restrict__ acl, uint64_t n,
-    uint8_t *__restrict__ out, const int32_t *__restrict__ status,
+    uint8_t *__restrict__ out, int32_t *__restrict__ status,
     const uint64_t *__restrict__ acl_pos, const uint64_t *__restrict__ payload_off,
     const uint64_t *__restrict__ out_off, uint64_t out_cap) {
     const uint32_t r = threadIdx.x & (G - 1);
@@ -239,6 +245,11 @@ HONU_DEV void k_encode_acl_grp_one(uint64_t i, const honu_meta *__restrict__ met
     const int32_t sti = status[i];
     const honu_meta &m = meta[i];
     const uint64_t na = m.acl_count, ao = m.acl_off;
+    // a carried list length (HONU_ACL_SIZED) sized the record: every entry is
+    // read below anyway, so the length is checked here (a row that lies gets
+    // HONU_ERR_INPUT; its range of the output is then unspecified)
+    const bool sized = (m.present & HONU_ACL_SIZED) != 0;
+    const uint64_t carried = m.acl_bytes;
     uint64_t pos;
     if constexpr (SELF) {
         const uint64_t beg = out_off[i], end = out_off[i + 1];
@@ -257,13 +268,27 @@ HONU_DEV void k_encode_acl_grp_one(uint64_t i, const honu_meta *__restrict__ met
         const uint64_t dlen = payload_off[i + 1] - payload_off[i];
         uint64_t miss = 0;  // nil entries
         for (uint64_t k = r; k < na; k += G) miss += acl[ao + k].present ? 0 : 1;
-        pos = (beg + 1 + uvarint_len(dlen) + dlen + t) | (grp_sum64<G>(miss) == 0 ? ACL_ALL_PRESENT : 0);
+        miss = grp_sum64<G>(miss);
+        if (sized && carried != 18 * (na - miss) + miss) {
+            if (r == 0) status[i] = HONU_ERR_INPUT;
+            return;
+        }
+        pos = (beg + 1 + uvarint_len(dlen) + dlen + t) | (miss == 0 ? ACL_ALL_PRESENT : 0);
     } else {
         pos = acl_pos[i];
         if (sti != HONU_OK || !na) return;
     }
     const honu_acl *A = acl + ao;
     const uint64_t P = pos & ~ACL_ALL_PRESENT;
+    if (!SELF && sized) {  // the lane encoder laid the list out by the carried length
+        uint64_t miss = 0;  // (the lines the chunks below read anyway)
+        for (uint64_t k = r; k < na; k += G) miss += A[k].present ? 0 : 1;
+        miss = grp_sum64<G>(miss);
+        if (carried != 18 * (na - miss) + miss) {
+            if (r == 0) status[i] = HONU_ERR_INPUT;
+            return;
+        }
+    }
     if (pos & ACL_ALL_PRESENT) {  // whole chunks [ceil16(P), floor16(E))
         // whole ACL_UNIT units on absolute addresses (lane.h writes the ends)
         const uint64_t ab = (uint64_t)out;
@@ -305,7 +330,7 @@ HONU_DEV void k_encode_acl_grp_one(uint64_t i, const honu_meta *__restrict__ met
 template <int G, bool SELF>
 __global__ __launch_bounds__(HONU_BLOCK) void k_encode_acl_grp(
     const honu_meta *__restrict__ meta, const honu_acl *__restrict__ acl, uint64_t n,
-    uint8_t *__restrict__ out, const int32_t *__restrict__ status,
+    uint8_t *__restrict__ out, int32_t *__restrict__ status,
     const uint64_t *__restrict__ acl_pos, const uint64_t *__restrict__ payload_off,
     const uint64_t *__restrict__ out_off, uint64_t out_cap) {
     for (uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G; i < n;
@@ -326,7 +351,7 @@ hipError_t launch_encode_sizes_grp(const honu_meta *meta, uint64_t var_len, cons
 }
 
 hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uint64_t n,
-                                 uint8_t *out, const int32_t *status, const uint64_t *acl_pos,
+                                 uint8_t *out, int32_t *status, const uint64_t *acl_pos,
                                  int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL((k_encode_acl_grp<GRP, false>), grp_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta, acl,
@@ -336,7 +361,7 @@ hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uin
 
 hipError_t launch_encode_acl_grp_self(const honu_meta *meta, const honu_acl *acl, const uint64_t *payload_off,
                                       uint64_t n, uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
-                                      const int32_t *status, int max_blocks, hipStream_t s) {
+                                      int32_t *status, int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL((k_encode_acl_grp<GRP, true>), grp_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta, acl,
                        n, out, status, nullptr, payload_off, out_off, out_cap);

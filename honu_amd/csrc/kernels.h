@@ -99,10 +99,12 @@ struct LaunchGeom {
                             // per-group / per-lane forms 1-4: DESIGN §3)
     uint32_t *tile_map;     // sweep-form tile -> segment map (context scratch)
     uint64_t tile_map_cap;
-    uint32_t *copy_tickets; // the copies' range-tail counters (copy.hip): encode, span, decode
+    uint32_t *copy_tickets; // the copies' range-tail counters (copy.hip): in the context's
+                            // geometry the ring's first line, in a launch's copy its own line
     int copy_steal;         // 1: range tails from the counters (default), 0: off
 };
-#define COPY_TICKET_STRIDE 32u  // uint32 words: one 128-byte line per kind of copy
+#define COPY_TICKET_STRIDE 32u  // uint32 words: one 128-byte line per copy launch
+#define COPY_TICKET_LINES 64u   // the ring: copy calls in flight at once on one context
 
 hipError_t launch_encode_copy(const LaunchGeom &g, const uint8_t *payload,
                               const uint64_t *payload_off, uint64_t n, uint8_t *out,
@@ -125,13 +127,13 @@ hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, co
                                    int32_t *status, uint64_t *acl_out, int max_blocks, int num_cu,
                                    const uint8_t *payload, hipStream_t s);
 hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uint64_t n,
-                                 uint8_t *out, const int32_t *status, const uint64_t *acl_pos,
+                                 uint8_t *out, int32_t *status, const uint64_t *acl_pos,
                                  int max_blocks, hipStream_t s);
 // the same with the lists placed by the kernel itself (no acl_pos), so that it
 // can run beside launch_encode_meta_lane
 hipError_t launch_encode_acl_grp_self(const honu_meta *meta, const honu_acl *acl, const uint64_t *payload_off,
                                       uint64_t n, uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
-                                      const int32_t *status, int max_blocks, hipStream_t s);
+                                      int32_t *status, int max_blocks, hipStream_t s);
 // header + Metadata tail, ACL entries included, one record per 16-lane group
 // (enc.hip; encode_variant 1, A/B build only)
 hipError_t launch_encode_tail_grp(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
@@ -158,13 +160,13 @@ hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint
                                uint64_t data_cap, DecodeScratch *scratch, uint64_t *offs,
                                uint64_t *totals, LbState *lb, uint64_t *lb_status,
                                uint64_t *lb_gstatus, uint64_t lb_words, int max_blocks, uint32_t *spec_seen,
-                               uint32_t *recoveries, bool allow_spec, bool inplace, bool inline_rec,
-                               int guard_blocks, hipStream_t s);
+                               uint32_t *recoveries, bool allow_spec, bool inplace, bool reg_inplace,
+                               bool inline_rec, int guard_blocks, hipStream_t s);
 
 hipError_t launch_decode_parse_win(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                    honu_meta *meta, honu_record_info *info,
                                    DecodeScratch *scratch, uint32_t *reg_inline, uint64_t *counts,
-                                   int max_blocks, bool inplace, hipStream_t s);
+                                   int max_blocks, bool inplace, bool reg_inplace, hipStream_t s);
 
 hipError_t launch_system_sizes(const honu_collection *rows, uint64_t var_len, const honu_acl *acl,
                                uint64_t acl_len, const uint32_t *reg, uint64_t reg_len,

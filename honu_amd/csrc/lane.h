@@ -410,71 +410,8 @@ static __device__ uint64_t g_enc_stamps[1 << 16][ENC_STAMPS];  // per translatio
 // encode of one record by one lane (object.go:24-45, metadata.go:108-200),
 // shared by the split kernels (lane.hip) and the fused kernel (fused.hip)
 // ------------------------------------------------------------------------
-HONU_DEV bool span_in(uint64_t off, uint64_t len, uint64_t var_len) {
-    return len == 0 || (off <= var_len && len <= var_len - off);
-}
 HONU_DEV uint64_t frame_len(uint64_t len) { return uvarint_len(len) + len; }
 HONU_DEV uint64_t ld64(const uint8_t *p) { return *reinterpret_cast<const uint64_t *>(p); }
-
-// HONU_OK, or the status of a record that cannot be encoded: HONU_ERR_PANIC
-// for Marshal(nil, ...) (nil deref in Size(), metadata.go:66), HONU_ERR_INPUT
-// for a span or list outside its arena.
-HONU_DEV int32_t encode_check(const honu_meta &m, uint64_t var_len, uint64_t acl_len,
-                              uint64_t reg_len) {
-    const uint32_t pr = m.present;
-    if (!(pr & HONU_HAS_META)) return HONU_ERR_PANIC;
-    bool ok = span_in(m.mime.off, m.mime.len, var_len);
-    if (pr & HONU_HAS_SCHEMA) ok = ok && span_in(m.schema_name.off, m.schema_name.len, var_len);
-    if (pr & HONU_HAS_PUBLISHER)
-        ok = ok && span_in(m.ip_address.off, m.ip_address.len, var_len) &&
-             span_in(m.user_agent.off, m.user_agent.len, var_len);
-    if (pr & HONU_HAS_ENCRYPTION)
-        ok = ok && span_in(m.public_key_id.off, m.public_key_id.len, var_len) &&
-             span_in(m.encryption_key.off, m.encryption_key.len, var_len) &&
-             span_in(m.hmac_secret.off, m.hmac_secret.len, var_len) &&
-             span_in(m.signature.off, m.signature.len, var_len);
-    const uint64_t na = m.acl_count, nr = m.regions_count;
-    const uint64_t ao = m.acl_off, ro = m.regions_off;
-    if (na) ok = ok && ao <= acl_len && na <= acl_len - ao;
-    if (nr) ok = ok && ro <= reg_len && nr <= reg_len - ro;
-    ok = ok && !(pr & HONU_ACL_INPLACE);  // a decode output row: its list is not in the table
-    return ok ? HONU_OK : HONU_ERR_INPUT;
-}
-
-// Encoded bytes of the Metadata tail (with its nil flag) except the ACL
-// entries themselves (1 byte per nil entry, 18 per present one): App. A.
-HONU_DEV uint64_t encode_tail_bytes_noacl(const honu_meta &m, const uint32_t *__restrict__ reg) {
-    const uint32_t pr = m.present;
-    const uint64_t na = m.acl_count, nr = m.regions_count, ro = m.regions_off;
-    uint64_t t = 1 + 32;  // meta flag, ObjectID, CollectionID
-    t += 1;               // Version flag
-    if (pr & HONU_HAS_VERSION)
-        t += uvarint_len(m.pid) + uvarint_len(m.vid) + uvarint_len(m.region) + 1 +
-             ((pr & HONU_HAS_PARENT) ? uvarint_len(m.parent_pid) + uvarint_len(m.parent_vid) : 0) +
-             1 + uvarint_len(zigzag(m.version_created));
-    t += 1;  // Schema flag
-    if (pr & HONU_HAS_SCHEMA)
-        t += frame_len(m.schema_name.len) + uvarint_len(m.schema_major) +
-             uvarint_len(m.schema_minor) + uvarint_len(m.schema_patch);
-    t += frame_len(m.mime.len) + 33;  // MIME, Owner, Group, Permissions
-    t += uvarint_len(na);
-    t += uvarint_len(nr);
-    for (uint64_t k0 = 0; k0 < nr; k0 += 8) {
-        uint32_t r8[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) r8[j] = k0 + j < nr ? reg[ro + k0 + j] : 0;
-#pragma unroll
-        for (int j = 0; j < 8; j++) t += k0 + j < nr ? uvarint_len(r8[j]) : 0;
-    }
-    t += 3;  // Publisher, Encryption, Compression flags
-    if (pr & HONU_HAS_PUBLISHER) t += 32 + frame_len(m.ip_address.len) + frame_len(m.user_agent.len);
-    if (pr & HONU_HAS_ENCRYPTION)
-        t += frame_len(m.public_key_id.len) + frame_len(m.encryption_key.len) +
-             frame_len(m.hmac_secret.len) + frame_len(m.signature.len) + 3;
-    if (pr & HONU_HAS_COMPRESSION) t += 1 + uvarint_len(zigzag(m.compression_level));
-    t += 1 + uvarint_len(zigzag(m.created)) + uvarint_len(zigzag(m.modified));
-    return t;
-}
 
 // The list kernel (k_encode_acl_grp) writes an all-present ACL list's whole
 // ACL_UNIT-byte units, this lane the list's bytes in the partial units at

@@ -169,17 +169,29 @@ HONU_DEV void lb_resolve(uint64_t *status, uint64_t t, uint32_t ep, const uint64
 // earlier groups, so no total waits on another: a prefix is two round trips
 // after the aggregates. Tile words keep their aggregates (no inclusive
 // prefixes are written).
+//
+// need (wave-uniform; both grouped forms): false for a tile that uses none of
+// its prefixes (a zero-copy tile with no table entry of its own, and not the
+// launch's last tile, which writes the totals): it does not wait for its
+// predecessors at all, and excl is then meaningless (the caller zeroes it). A
+// group's last tile still publishes the group's aggregate (it waits only for
+// its own group's tile aggregates); in the ticket form it publishes the
+// group's inclusive prefix only when it needed its own, so a later tile that
+// needs offsets may sum further back over aggregates (64 groups per round
+// trip). With the ACL and region lists returned in place a zero-copy decode's
+// tiles need nothing (fused.hip).
 constexpr uint32_t LB_GROUPS = 64;
 template <int K>
 HONU_DEV void lb_resolve_grouped(uint64_t *status, uint64_t *gstatus, uint64_t t, uint64_t ntiles,
-                                 uint32_t ep, const uint64_t (&agg)[K], uint64_t (&excl)[K]) {
+                                 uint32_t ep, const uint64_t (&agg)[K], uint64_t (&excl)[K],
+                                 bool need = true) {
     const uint32_t lane = lane_id();
     const uint64_t g = t / HONU_WAVE, r = t % HONU_WAVE;
     const bool closer = r == HONU_WAVE - 1 && t + 1 < ntiles;  // the last group's total is not needed
     // wave-uniform bit masks of the parts still missing: bit c this group's
     // tiles before t (r of them), bit K + c the totals of groups 0 .. g - 1
-    uint32_t todo = (1u << K) - 1;
-    if (g) todo |= ((1u << K) - 1) << K;
+    uint32_t todo = need || closer ? (1u << K) - 1 : 0;
+    if (g && need) todo |= ((1u << K) - 1) << K;
 #pragma unroll
     for (int c = 0; c < K; c++) excl[c] = 0;
     for (;;) {
@@ -215,12 +227,13 @@ HONU_DEV void lb_resolve_grouped(uint64_t *status, uint64_t *gstatus, uint64_t t
 // trips where the tile-level look-back took two or three.
 template <int K>
 HONU_DEV void lb_resolve_grouped_lb(uint64_t *status, uint64_t *gstatus, uint64_t t, uint64_t ntiles,
-                                    uint32_t ep, const uint64_t (&agg)[K], uint64_t (&excl)[K]) {
+                                    uint32_t ep, const uint64_t (&agg)[K], uint64_t (&excl)[K],
+                                    bool need = true) {
     const uint32_t lane = lane_id();
     const uint64_t g = t / HONU_WAVE, r = t % HONU_WAVE;
     const bool closer = r == HONU_WAVE - 1 && t + 1 < ntiles;
-    uint32_t todo = (1u << K) - 1;              // bit c: this group's tiles before t
-    if (g) todo |= ((1u << K) - 1) << K;        // bit K + c: the groups before g
+    uint32_t todo = need || closer ? (1u << K) - 1 : 0;  // bit c: this group's tiles before t
+    if (g && need) todo |= ((1u << K) - 1) << K;         // bit K + c: the groups before g
     int64_t top[K];
     uint64_t in_sum[K];
 #pragma unroll
@@ -259,7 +272,7 @@ HONU_DEV void lb_resolve_grouped_lb(uint64_t *status, uint64_t *gstatus, uint64_
         if (!todo) break;
         __builtin_amdgcn_s_sleep(1);
     }
-    if (closer) {  // the group's inclusive prefix: this tile's own inclusive one
+    if (closer && need) {  // the group's inclusive prefix: this tile's own inclusive one
 #pragma unroll
         for (int c = 0; c < K; c++)
             if (lane == (uint32_t)c) lb_store(gstatus + g * K + c, lb_word(2, ep, excl[c] + agg[c]));

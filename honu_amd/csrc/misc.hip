@@ -99,7 +99,9 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_digest(const uint8_t *__restrict
 // compared; their bytes are. ACL entries and regions are compared entry by
 // entry through both rows' list offsets; a list the decode returned in place
 // (HONU_ACL_INPLACE, allowed only when every source entry is present) is
-// compared with its 18-byte encodings in the records arena.
+// compared with its 18-byte encodings in the records arena, a region list
+// returned in place (HONU_REGIONS_INPLACE, any non-empty list) by decoding its
+// uvarints there (lani.DecodeUint32: <= 5 bytes, truncated to uint32).
 // ------------------------------------------------------------------------
 constexpr uint32_t G_ALWAYS = 0, G_IGNORE = 0xFFFFFFFFu, G_ZERO = 0xFFFFFFFEu;
 
@@ -163,8 +165,11 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_verify_decoded(
         bool any_nil = false;
         for (uint64_t j = lane; pr && j < S.acl_count; j += HONU_WAVE) any_nil |= !src_acl[S.acl_off + j].present;
         const bool all_present = pr && S.acl_count && !__ballot(any_nil);
-        const bool inpl = all_present && D.present == (pr | HONU_ACL_INPLACE);
-        if (D.present != pr && !inpl) bad |= HONU_VERIFY_PRESENT;
+        // the in-place region bit: allowed on a non-empty list only
+        const bool rinpl = pr && S.regions_count && (D.present & HONU_REGIONS_INPLACE);
+        const uint32_t dpr = D.present & ~(rinpl ? (uint32_t)HONU_REGIONS_INPLACE : 0u);
+        const bool inpl = all_present && dpr == (pr | HONU_ACL_INPLACE);
+        if (dpr != pr && !inpl) bad |= HONU_VERIFY_PRESENT;
         bool row_bad = false;
         for (uint32_t b = lane; b < sizeof(honu_meta); b += HONU_WAVE) {
             const uint32_t g = row_gate(b);
@@ -202,8 +207,23 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_verify_decoded(
             }
             if (__ballot(acl_bad)) bad |= HONU_VERIFY_ACL;
             bool reg_bad = false;
-            for (uint64_t j = lane; j < S.regions_count; j += HONU_WAVE)
+            for (uint64_t j = lane; !rinpl && j < S.regions_count; j += HONU_WAVE)
                 reg_bad |= src_reg[S.regions_off + j] != dec_reg[D.regions_off + j];
+            if (rinpl && lane == 0) {  // the list's uvarints, one after the other
+                uint64_t p = D.regions_off;
+                for (uint64_t j = 0; j < S.regions_count && !reg_bad; j++) {
+                    uint64_t v = 0;
+                    uint32_t k = 0, sh = 0;
+                    for (; k < 5; k++) {
+                        const uint32_t b = rec[p + k];
+                        v |= (uint64_t)(b & 0x7F) << sh;
+                        sh += 7;
+                        if (!(b & 0x80)) break;
+                    }
+                    reg_bad |= k == 5 || (uint32_t)v != src_reg[S.regions_off + j];
+                    p += k + 1;
+                }
+            }
             if (__ballot(reg_bad)) bad |= HONU_VERIFY_REGIONS;
         }
         if (lane == 0) mismatch[i] = bad;

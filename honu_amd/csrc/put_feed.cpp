@@ -228,7 +228,8 @@ static int32_t put_plan(const honu_put_feed *f, const honu_meta *row, const uint
             if (sv.len && (!var || sv.off > var_len || sv.len > var_len - sv.off)) return HONU_ERR_INPUT;
             p.span_bytes += sv.len;
         }
-        if (row->present & HONU_ACL_INPLACE) return HONU_ERR_INPUT;  // a decode output row (table form only)
+        if (row->present & (HONU_ACL_INPLACE | HONU_REGIONS_INPLACE))
+            return HONU_ERR_INPUT;  // a decode output row (table forms only)
         p.nacl = row->acl_count;
         p.nreg = row->regions_count;
         if (p.nacl && (!acl || row->acl_off > acl_len || p.nacl > acl_len - row->acl_off))
@@ -267,6 +268,14 @@ static void put_fill(Slot &s, uint64_t idx, const PutPlan &p, const honu_meta *r
     }
     if (p.nacl) std::memcpy(s.h_acl + p.acl_at, acl + row->acl_off, sizeof(honu_acl) * p.nacl);
     if (p.nreg) std::memcpy(s.h_reg + p.reg_at, regions + row->regions_off, 4 * p.nreg);
+    if (p.nacl && !(w.present & HONU_ACL_SIZED)) {
+        // the list's encoded length, from the entries just copied (HONU_ACL_SIZED:
+        // the size pass then reads no ACL entry; a row that carries one keeps it)
+        uint64_t nb = 0;
+        for (uint64_t j = 0; j < p.nacl; j++) nb += acl[row->acl_off + j].present ? 18 : 1;
+        w.acl_bytes = nb;
+        w.present |= HONU_ACL_SIZED;
+    }
     w.acl_off = p.nacl ? p.acl_at : 0;
     w.regions_off = p.nreg ? p.reg_at : 0;
     if (data_len) std::memcpy(s.h_pay + p.pay_at, data, data_len);

@@ -291,7 +291,8 @@ struct NoEarly {
 // What the walk of one record leaves in the lane's registers.
 struct WinParse {
     int st;             // Metadata() status; HONU_SKIP for a lane past n
-    uint64_t nacl, nreg;
+    uint64_t nacl;
+    uint64_t nreg;      // region table entries: the list's length, 0 for a list returned in place
     uint64_t ntab;      // ACL table entries: nacl, or 0 for a list returned in place
     uint64_t acl_pos;   // first ACL entry flag, | GRP_ACL_FAST when every entry is present
     uint64_t reg_pos;   // first region varint, | GRP_REG_INLINE when nreg <= REG_INLINE
@@ -335,15 +336,19 @@ HONU_DEV void tile_head_bytes(const uint8_t *__restrict__ rec, TileHead &H) {
 // of record i0 + lane, the lani walk of metadata.go:202-302. Wave-uniform
 // call (every lane of the wave, i0 the same): the window refills need the
 // whole wave. H: the tile's bounds and header bytes (tile_head_*). The row
-// goes to R (RegRow, regions_off not yet set; acl_off only for a list returned
-// in place). inplace (wave-uniform): a list whose entries are all present is
-// returned in place (HONU_ACL_INPLACE, acl_off = its absolute position, no
-// table entries); with early.spec_acl that is speculated like the rest of the
-// list's layout and the caller checks the flags.
+// goes to R (RegRow; acl_off / regions_off only for lists returned in place,
+// the table forms' offsets are the caller's). inplace (wave-uniform): a list
+// whose entries are all present is returned in place (HONU_ACL_INPLACE,
+// acl_off = its absolute position, no table entries); with early.spec_acl
+// that is speculated like the rest of the list's layout and the caller checks
+// the flags. reg_inplace: every non-empty region list is returned in place
+// (HONU_REGIONS_INPLACE, regions_off = its first varint's absolute position;
+// every varint still validated here), so P.nreg, the region TABLE entries, is
+// 0 and nothing is kept in P.regs.
 template <class RowT, class EarlyT>
 HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restrict__ rec,
                        uint64_t n, const TileHead &H, RowT &R, WinParse &P, EarlyT &early,
-                       bool inplace) {
+                       bool inplace, bool reg_inplace) {
 #define OFF(f) ((int)offsetof(honu_meta, f))
 #define STEP(x)                      \
     do {                             \
@@ -550,21 +555,29 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
         if (st == HONU_OK && nreg > GO_MAX_ALLOC / 4) st = HONU_ERR_PANIC;  // make(Regions, n)
         pr |= HONU_REGIONS_NONNIL;
         reg_pos = D.p;
-#pragma unroll
-        for (int k = 0; k < REG_INLINE; k++) {
-            if ((uint64_t)k < nreg) {
-                STEP(D.u32(u));
-                P.regs[k] = u;
+        if (reg_inplace) {  // region.go:154-169 without the copy: validated, not kept
+            for (uint64_t k = 0; k < nreg && st == HONU_OK; k++) STEP(D.u32(u));
+            if (st == HONU_OK && nreg) {
+                pr |= HONU_REGIONS_INPLACE;
+                R.u64(OFF(regions_off), reg_pos);
             }
+        } else {
+#pragma unroll
+            for (int k = 0; k < REG_INLINE; k++) {
+                if ((uint64_t)k < nreg) {
+                    STEP(D.u32(u));
+                    P.regs[k] = u;
+                }
+            }
+            for (uint64_t k = REG_INLINE; k < nreg && st == HONU_OK; k++) STEP(D.u32(u));
         }
-        for (uint64_t k = REG_INLINE; k < nreg && st == HONU_OK; k++) STEP(D.u32(u));
         if (nreg <= REG_INLINE) reg_pos |= GRP_REG_INLINE;
         R.u64(OFF(regions_count), nreg);
     }
     // both list counts are known here; a later field can still fail the
     // record (its counts then become 0): the early hook publishes them
     // tentatively (fused.hip speculative decode)
-    early.counts(hm && st == HONU_OK && !inpl ? nacl : 0, hm && st == HONU_OK ? nreg : 0,
+    early.counts(hm && st == HONU_OK && !inpl ? nacl : 0, hm && st == HONU_OK && !reg_inplace ? nreg : 0,
                  (P.data_len + 15) & ~15ull);
     if (hm) {
         STEP(D.boolean(f));                                 // :271 Publisher
@@ -619,7 +632,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
     P.st = st;
     P.nacl = nacl;
     P.ntab = inpl ? 0 : nacl;
-    P.nreg = nreg;
+    P.nreg = reg_inplace ? 0 : nreg;  // region table entries
     P.acl_pos = acl_pos;
     P.reg_pos = reg_pos;
 #undef STEP

@@ -20,7 +20,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_win(
     const uint8_t *__restrict__ rec, const uint64_t *__restrict__ rec_off, uint64_t n,
     honu_meta *__restrict__ meta, honu_record_info *__restrict__ info,
     DecodeScratch *__restrict__ scratch, uint32_t *__restrict__ reg_inline,
-    uint64_t *__restrict__ counts, bool inplace) {
+    uint64_t *__restrict__ counts, bool inplace, bool reg_inplace) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * WIN_WAVE_BYTES];
     const uint32_t wv = threadIdx.x / HONU_WAVE;
     uint8_t *ws = smem + wv * WIN_WAVE_BYTES;
@@ -33,7 +33,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_win(
         tile_head_bytes(rec, H);
         RegRow R;
         NoEarly none;
-        win_walk(i0, ws, rec, n, H, R, P, none, inplace);
+        win_walk(i0, ws, rec, n, H, R, P, none, inplace, reg_inplace);
         rows_out(ws, R, i0, n, meta);
         const uint64_t i = i0 + lane_id();
         if (i >= n) continue;
@@ -45,7 +45,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_parse_win(
         for (int k = 0; k < 8; k++)
             if ((uint64_t)k < P.nreg) reg_inline[8 * i + k] = P.regs[k];
         counts[3 * i + 0] = P.ntab;  // 0 for a list returned in place
-        counts[3 * i + 1] = P.nreg;
+        counts[3 * i + 1] = P.nreg;  // 0 for a list returned in place
         counts[3 * i + 2] = (P.data_len + 15) & ~15ull;
     }
 }
@@ -58,11 +58,11 @@ static dim3 win_grid(uint64_t n, int cap) {
 hipError_t launch_decode_parse_win(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                    honu_meta *meta, honu_record_info *info,
                                    DecodeScratch *scratch, uint32_t *reg_inline, uint64_t *counts,
-                                   int max_blocks, bool inplace, hipStream_t s) {
+                                   int max_blocks, bool inplace, bool reg_inplace, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_decode_parse_win, win_grid(n, max_blocks),
                        dim3(HONU_BLOCK), 0, s, rec, rec_off, n, meta, info, scratch, reg_inline,
-                       counts, inplace);
+                       counts, inplace, reg_inplace);
     return hipGetLastError();
 }
 

@@ -26,19 +26,19 @@ META_DTYPE = np.dtype(
             "present", "permissions", "flags", "tombstone", "compression_alg",
             "sealing_alg", "encryption_alg", "signature_alg", "region", "vid", "pid",
             "parent_pid", "parent_vid", "version_created", "schema_major", "schema_minor",
-            "schema_patch", "compression_level", "created", "modified", "object_id",
+            "schema_patch", "compression_level", "created", "modified", "acl_bytes", "object_id",
             "collection_id", "owner", "group", "publisher_id", "client_id", "schema_name",
             "mime", "ip_address", "user_agent", "public_key_id", "encryption_key",
             "hmac_secret", "signature", "acl_off", "acl_count", "regions_off", "regions_count",
         ],
         "formats": [
             "<u4", "u1", "u1", "u1", "u1", "u1", "u1", "u1", "<u4", "<u8", "<u4", "<u4", "<u8",
-            "<i8", "<u4", "<u4", "<u4", "<i8", "<i8", "<i8", ("u1", 16), ("u1", 16), ("u1", 16),
+            "<i8", "<u4", "<u4", "<u4", "<i8", "<i8", "<i8", "<u8", ("u1", 16), ("u1", 16), ("u1", 16),
             ("u1", 16), ("u1", 16), ("u1", 16), SPAN, SPAN, SPAN, SPAN, SPAN, SPAN, SPAN, SPAN,
             "<u8", "<u8", "<u8", "<u8",
         ],
         "offsets": [
-            0, 4, 5, 6, 7, 8, 9, 10, 12, 16, 24, 28, 32, 40, 48, 52, 56, 64, 72, 80, 96, 112,
+            0, 4, 5, 6, 7, 8, 9, 10, 12, 16, 24, 28, 32, 40, 48, 52, 56, 64, 72, 80, 88, 96, 112,
             128, 144, 160, 176, 192, 208, 224, 240, 256, 272, 288, 304, 320, 328, 336, 344,
         ],
         "itemsize": 352,
@@ -66,6 +66,8 @@ HAS_ENCRYPTION = 1 << 5
 HAS_COMPRESSION = 1 << 6
 REGIONS_NONNIL = 1 << 7
 ACL_INPLACE = 1 << 8  # decode output: the ACL list in place in the records arena (honu_codec.h)
+REGIONS_INPLACE = 1 << 9  # decode output: the region list in place in the records arena
+ACL_SIZED = 1 << 10  # encode input: acl_bytes holds the ACL list's encoded length (honu_codec.h)
 
 SPAN_FIELDS = ("schema_name", "mime", "ip_address", "user_agent", "public_key_id",
                "encryption_key", "hmac_secret", "signature")
@@ -209,6 +211,10 @@ def pack_common(r, m, span, acl_rows: list, regions: list) -> int:
         r["acl_off"], r["acl_count"] = len(acl_rows), len(m.ACL)
         for a in m.ACL:
             acl_rows.append(None if a is None else (_ulid(a.ClientID), a.Permissions))
+        if "acl_bytes" in r.dtype.names:  # honu_meta: the list's encoded length, as the
+            # binding's flatten carries it (HONU_ACL_SIZED: the size pass reads no entry)
+            r["acl_bytes"] = sum(1 if a is None else 18 for a in m.ACL)
+            pr |= ACL_SIZED
     if m.WriteRegions:
         r["regions_off"], r["regions_count"] = len(regions), len(m.WriteRegions)
         regions.extend(m.WriteRegions)
@@ -294,7 +300,8 @@ def unpack_row(row, arena, acl_table=None, regions_table=None) -> Metadata:
     """Rebuild a Metadata from a decoded row; spans index `arena`, lists the
     decoded tables, or `arena` for an ACL list returned in place
     (ACL_INPLACE: entry j = the 18 bytes 01 | ClientID | Permissions at
-    acl_off + 18 j). Mirrors the nil/empty rules of the Go decoder
+    acl_off + 18 j) or a region list returned in place (REGIONS_INPLACE: the
+    uvarints from regions_off). Mirrors the nil/empty rules of the Go decoder
     (lani/decode.go:37-39, metadata.go:254, region.go:160)."""
     pr = int(row["present"])
     m = Metadata()
@@ -331,6 +338,28 @@ def acl_inplace_entries(arena, off: int, count: int) -> list:
     return out
 
 
+def regions_inplace_values(arena, off: int, count: int) -> list:
+    """The WriteRegions of a row returned in place (REGIONS_INPLACE): what
+    Regions.Decode builds from those bytes (region.go:154-169), each uvarint
+    read as lani.DecodeUint32 does (at most 5 bytes, truncated to uint32,
+    decode.go:127-146; the GPU decode has validated every one of them)."""
+    arena = memoryview(arena)
+    out, p = [], off
+    for j in range(count):
+        v, sh = 0, 0
+        for k in range(5):
+            b = arena[p + k]
+            v |= (b & 0x7F) << sh
+            sh += 7
+            if not b & 0x80:
+                break
+        else:
+            raise ValueError("in-place region %d is not a 5-byte uvarint" % j)
+        out.append(v & 0xFFFFFFFF)
+        p += k + 1
+    return out
+
+
 def unpack_common(row, m, sb, ss, acl_table, regions_table, arena=None):
     """Inverse of pack_common on a decoded row (Go decoder nil/empty rules)."""
     pr = int(row["present"])
@@ -356,7 +385,9 @@ def unpack_common(row, m, sb, ss, acl_table, regions_table, arena=None):
             m.ACL.append(AccessControl(bytes(a["client_id"]), int(a["permissions"]))
                          if a["present"] else None)
     nr = int(row["regions_count"])
-    if pr & REGIONS_NONNIL or nr:
+    if nr and pr & REGIONS_INPLACE:
+        m.WriteRegions = regions_inplace_values(arena, int(row["regions_off"]), nr)
+    elif pr & REGIONS_NONNIL or nr:
         base = int(row["regions_off"])
         m.WriteRegions = [int(x) for x in regions_table[base:base + nr]] if nr else []
     if pr & HAS_PUBLISHER:

@@ -41,7 +41,8 @@
 extern "C" {
 #endif
 
-#define HONU_ABI_VERSION 5u  /* 5: honu_encode_*_units; 4: ACL lists returned in place (HONU_ACL_INPLACE) */
+#define HONU_ABI_VERSION 6u  /* 6: region lists returned in place (HONU_REGIONS_INPLACE);
+                                5: honu_encode_*_units; 4: ACL lists returned in place (HONU_ACL_INPLACE) */
 #define HONU_STORAGE_VERSION 1u /* object.StorageVersion, object.go:14 */
 #define HONU_ULID_LEN 16
 #define HONU_KEY_LEN 29         /* keys.keySize, keys/keys.go:14 */
@@ -94,8 +95,12 @@ enum {
     HONU_HAS_COMPRESSION = 1u << 6, /* Metadata.Compression  metadata.go:30 */
     HONU_REGIONS_NONNIL = 1u << 7,  /* set by decode: Regions.Decode always makes a
                                        (possibly empty) slice, region.go:160 */
-    HONU_ACL_INPLACE = 1u << 8      /* set by decode (honu_meta only): the ACL list is
+    HONU_ACL_INPLACE = 1u << 8,     /* set by decode (honu_meta only): the ACL list is
                                        returned in place, see honu_meta.acl_off */
+    HONU_REGIONS_INPLACE = 1u << 9, /* set by decode (honu_meta only): the region list
+                                       is returned in place, see honu_meta.regions_off */
+    HONU_ACL_SIZED = 1u << 10       /* encode input (honu_meta only): acl_bytes holds the
+                                       ACL list's encoded length, see honu_meta.acl_bytes */
 };
 
 /* One metadata.Metadata (metadata.go:17-35) flattened into a fixed 352-byte
@@ -117,8 +122,31 @@ enum {
  *           Go copies every entry into a new *AccessControl either way
  *           (metadata.go:254-266); the in-place form leaves that copy to the
  *           binding, as Data() and the string spans already do.
- *           Encode input rows must use the table form: a row with
- *           HONU_ACL_INPLACE set gets HONU_ERR_INPUT from honu_encode_sizes.
+ *           The region list likewise:
+ *           - in place (HONU_REGIONS_INPLACE set; the default, context param
+ *             "regions_inplace" 1, every non-empty list): regions_off is the
+ *             ABSOLUTE offset in the records arena of the first region's
+ *             uvarint; the regions_count uvarints follow back to back, each
+ *             decoded as lani.DecodeUint32 does (at most 5 bytes, the value
+ *             truncated to uint32: decode.go:127-146). The decode has already
+ *             validated every one of them (a bad varint fails the record), so
+ *             the binding's Regions.Decode loop (region.go:154-169) cannot fail;
+ *           - table (HONU_REGIONS_INPLACE clear, regions_count > 0; every list
+ *             when "regions_inplace" is 0): regions_off indexes the uint32
+ *             output region table.
+ *           In-place lists and spans point into the records arena: the row is
+ *           valid while that arena is. Encode input rows must use the table
+ *           forms: a row with HONU_ACL_INPLACE or HONU_REGIONS_INPLACE set gets
+ *           HONU_ERR_INPUT from honu_encode_sizes.
+ *   encode, HONU_ACL_SIZED (optional, what a binding's flatten sets while it
+ *           copies m.ACL): acl_bytes = sum over the list of 18 per present
+ *           entry and 1 per nil one (acls.go:26-39, encode.go:210-226), so the
+ *           size pass reads no ACL table entry (the list kernel reads every
+ *           entry anyway and checks the length: a row whose acl_bytes is not
+ *           the list's length gets HONU_ERR_INPUT from the records call and
+ *           its range of the output holds unspecified bytes; a value outside
+ *           [acl_count, 18 * acl_count] is rejected by honu_encode_sizes).
+ *           Without the bit the size pass reads the list from the table.
  * Times are Go UnixNano with 0 <=> time.Time{}.IsZero() (lani/encode.go:201-206,
  * decode.go:224-237). Fields of absent (nil) sub-structs are zero on decode. */
 typedef struct honu_meta {
@@ -144,7 +172,8 @@ typedef struct honu_meta {
     int64_t compression_level;   /*  64 Compression.Level */
     int64_t created;             /*  72 Metadata.Created */
     int64_t modified;            /*  80 Metadata.Modified */
-    uint64_t _pad2;              /*  88 */
+    uint64_t acl_bytes;          /*  88 encode input with HONU_ACL_SIZED: the ACL
+                                        list's encoded length; 0 on decode */
     uint8_t object_id[16];       /*  96 Metadata.ObjectID */
     uint8_t collection_id[16];   /* 112 Metadata.CollectionID */
     uint8_t owner[16];           /* 128 Metadata.Owner */
@@ -162,7 +191,8 @@ typedef struct honu_meta {
     uint64_t acl_off;            /* 320 first entry in the ACL table, or (decode,
                                         HONU_ACL_INPLACE) in the records arena */
     uint64_t acl_count;          /* 328 len(Metadata.ACL); 0 <=> nil */
-    uint64_t regions_off;        /* 336 first entry in the region table */
+    uint64_t regions_off;        /* 336 first entry in the region table, or (decode,
+                                        HONU_REGIONS_INPLACE) in the records arena */
     uint64_t regions_count;      /* 344 len(Metadata.WriteRegions) */
 } honu_meta;                     /* 352 */
 
@@ -196,10 +226,14 @@ typedef struct honu_ctx honu_ctx;
 /* Create a context on HIP device `device` with scratch for batches of up to
  * `max_records` records (scan partials, decode list positions). Allocation
  * happens here and only here. Returns NULL and sets *err on failure.
- * The scratch is per context: calls that use it (scan, decode, and the payload
- * copies of one kind — honu_encode_payloads*, honu_decode_payloads,
- * honu_decode_data — with their range-tail counters, param "copy_steal")
- * issued on different streams concurrently need one context each. Arenas: the records
+ * The scratch is per context: calls that use it (scans, decodes and the decode
+ * payload copies, which read the decode's scratch) issued on different
+ * streams concurrently need one context each. The encode payload copies
+ * (honu_encode_payloads*) use none and may run concurrently on one context:
+ * every copy call takes its own range-tail counter line from a ring of 64
+ * (param "copy_steal"), so up to 64 copies may be in flight at once on one
+ * context. The library reads no environment variable: a
+ * context is configured through honu_ctx_set_param only. Arenas: the records
  * arena, the materialised data arena and row arrays must be 16-byte aligned,
  * ACL and region tables 4-byte aligned (hipMalloc gives 256). */
 honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err);
@@ -240,13 +274,18 @@ int32_t honu_ctx_reset(honu_ctx *ctx, void *stream);
  * beside the header/tail encoder, forked from and joined back into the
  * caller's stream by events; 0 after it; 2, the default, forks when
  * "lane_blocks" caps the encoder's grid and the caller's stream has neither a
- * CU mask nor a non-default priority, which the fork's stream would escape). Also
- * settable at context creation through the environment (HONU_COPY_BLOCKS,
- * HONU_RECORD_BLOCKS, HONU_LANE_BLOCKS, HONU_COPY_VARIANT, HONU_RECORD_VARIANT,
- * HONU_ENCODE_VARIANT). "acl_inplace" (1 default, 0 off): the decode calls
+ * CU mask nor a non-default priority, which the fork's stream would escape).
+ * "acl_inplace" (1 default, 0 off): the decode calls
  * (honu_decode_parse/fill/tables/records/batch) return an ACL list whose
  * entries are all present in place (HONU_ACL_INPLACE, see honu_meta) instead
  * of copying it into the ACL table; 0 returns every list in the table.
+ * "regions_inplace" (1 default, 0 off): the same calls return every
+ * non-empty region list in place (HONU_REGIONS_INPLACE) instead of in the
+ * region table; 0 returns every list in the table. With both in place a
+ * zero-copy batch whose ACL lists hold no nil entry writes no table entry,
+ * and the single-launch decode's 64-record tiles then need no offsets from
+ * their predecessors (only the batch's last tile resolves them, for
+ * d_totals).
  * "inline_recovery" (0 default, 1 on): a speculative single-launch decode
  * with more 64-record tiles than resident waves redoes a misspeculated batch
  * inside the same launch instead of in a guarded second launch (one-wave
@@ -364,8 +403,10 @@ int32_t honu_decode_parse(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d
  * 16-byte aligned offset in d_data (d_info[i].data_off is then relative to
  * d_data) and copy the payloads there (honu_decode_payloads). d_totals
  * (device, 3 x u64) receives the totals the batch needs: ACL table entries
- * (lists returned in place take none), region entries, data-arena bytes (the
- * latter also in zero-copy mode). Records whose
+ * (lists returned in place take none), region table entries (likewise),
+ * data-arena bytes (the latter also in zero-copy mode). Rows returned with
+ * in-place lists (and every span) point into d_rec: keep the records arena
+ * alive while the rows are used. Records whose
  * outputs do not fit get HONU_ERR_CAPACITY in meta_status / data_status. */
 int32_t honu_decode_fill(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t *d_rec_off,
                          uint64_t n, honu_meta *d_meta, honu_record_info *d_info,

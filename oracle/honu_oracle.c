@@ -178,7 +178,13 @@ static int encode_meta(owriter *w, const honu_meta *m, const uint8_t *var, uint6
     if (m->regions_count &&
         (m->regions_off > regions_len || m->regions_count > regions_len - m->regions_off))
         bad = 1;
-    if (m->present & HONU_ACL_INPLACE) bad = 1; /* a decode output row: encode takes the table form */
+    /* a decode output row: encode takes the table forms */
+    if (m->present & (HONU_ACL_INPLACE | HONU_REGIONS_INPLACE)) bad = 1;
+    /* a carried list length (HONU_ACL_SIZED) must lie in [count, 18 count]
+     * (include/honu_codec.h; the exact check: oracle_marshal_batch) */
+    if ((m->present & HONU_ACL_SIZED) &&
+        (m->acl_bytes < m->acl_count || m->acl_bytes > 18 * m->acl_count))
+        bad = 1;
     if (bad) return HONU_ERR_INPUT;
 
     w_bool(w, 1);                         /* EncodeStruct(meta) flag, encode.go:210-216 */
@@ -380,10 +386,14 @@ typedef struct {
 
 #define TRY(x) do { int st_ = (x); if (st_) return st_; } while (0)
 
-/* Metadata.Decode (metadata.go:202-302) after its nil flag. acl_inplace: a
- * list whose entries are all present is returned in place (HONU_ACL_INPLACE,
- * acl_off = absolute offset of its first entry) instead of in the table. */
-static int decode_meta_body(oreader *r, uint64_t base, honu_meta *m, olists *L, int acl_inplace) {
+/* Metadata.Decode (metadata.go:202-302) after its nil flag. forms &
+ * ORACLE_ACL_INPLACE: a list whose entries are all present is returned in
+ * place (HONU_ACL_INPLACE, acl_off = absolute offset of its first entry)
+ * instead of in the table; forms & ORACLE_REGIONS_INPLACE: a non-empty region
+ * list is returned in place (HONU_REGIONS_INPLACE, regions_off = absolute
+ * offset of its first uvarint; every uvarint decoded and checked as below). */
+static int decode_meta_body(oreader *r, uint64_t base, honu_meta *m, olists *L, int forms) {
+    const int acl_inplace = forms & ORACLE_ACL_INPLACE, reg_inplace = forms & ORACLE_REGIONS_INPLACE;
     int b;
     TRY(r_ulid(r, m->object_id));                    /* :210 */
     TRY(r_ulid(r, m->collection_id));                /* :214 */
@@ -452,14 +462,20 @@ static int decode_meta_body(oreader *r, uint64_t base, honu_meta *m, olists *L, 
     if (nreg > GO_MAX_ALLOC / 4) return HONU_ERR_PANIC; /* make(Regions, length) */
     m->present |= HONU_REGIONS_NONNIL;
     m->regions_off = L->reg_n;
+    const uint64_t reg_at = base + r->i;
     for (uint64_t i = 0; i < nreg; i++) {
         uint32_t v;
         TRY(r_u32(r, &v));
+        if (reg_inplace) continue;  /* validated; the list stays where it is */
         if (L->reg_n < L->reg_cap) L->reg_out[L->reg_n] = v;
         L->reg_n++;
     }
     m->regions_count = nreg;
     if (nreg == 0) m->regions_off = 0;
+    else if (reg_inplace) {
+        m->present |= HONU_REGIONS_INPLACE;
+        m->regions_off = reg_at;
+    }
     TRY(r_bool(r, &b));                              /* :271 DecodeStruct(Publisher) */
     if (b) {                                         /* provenance.go:59-79 */
         m->present |= HONU_HAS_PUBLISHER;
@@ -510,7 +526,7 @@ static void data_length(const uint8_t *o, uint64_t len, int64_t *d, int64_t *b) 
 void oracle_decode(const uint8_t *o, uint64_t len, uint64_t base, honu_meta *m,
                    honu_record_info *info, honu_acl *acl_out, uint64_t acl_cap,
                    uint32_t *regions_out, uint64_t regions_cap, uint64_t *acl_n,
-                   uint64_t *regions_n, int acl_inplace) {
+                   uint64_t *regions_n, int forms) {
     memset(m, 0, sizeof *m);
     memset(info, 0, sizeof *info);
     *acl_n = 0;
@@ -543,7 +559,7 @@ void oracle_decode(const uint8_t *o, uint64_t len, uint64_t base, honu_meta *m,
     int st = r_bool(&r, &present);                   /* DecodeStruct(meta) :78 */
     if (st == HONU_OK && present) {
         m->present = HONU_HAS_META;
-        st = decode_meta_body(&r, base + t, m, &L, acl_inplace);
+        st = decode_meta_body(&r, base + t, m, &L, forms);
     }
     info->meta_status = st;
     if (st != HONU_OK) {
@@ -557,6 +573,14 @@ void oracle_decode(const uint8_t *o, uint64_t len, uint64_t base, honu_meta *m,
 /* ===================================================================== */
 /* Batch drivers                                                          */
 /* ===================================================================== */
+
+/* The ACL list's encoded length from the table: 18 per present entry, 1 per
+ * nil one (acls.go:26-39, encode.go:210-226). */
+static uint64_t acl_list_bytes(const honu_meta *m, const honu_acl *acl) {
+    uint64_t b = 0;
+    for (uint64_t j = 0; j < m->acl_count; j++) b += acl[m->acl_off + j].present ? 18 : 1;
+    return b;
+}
 
 int oracle_marshal_batch(const honu_meta *meta, const uint8_t *var, uint64_t var_len,
                          const honu_acl *acl, uint64_t acl_len, const uint32_t *regions,
@@ -572,12 +596,27 @@ int oracle_marshal_batch(const honu_meta *meta, const uint8_t *var, uint64_t var
         /* size pass: a record that cannot be encoded (PANIC, INPUT) has size 0 */
         int st = oracle_marshal(&meta[i], var, var_len, acl, acl_len, regions, regions_len, data,
                                 dlen, NULL, 0, &sz);
+        /* a row carrying its ACL list's length (HONU_ACL_SIZED) is sized by
+         * that length without reading the table (honu_encode_sizes); one whose
+         * length is not the list's gets HONU_ERR_INPUT from the encode and its
+         * range stays unwritten here (unspecified bytes on the GPU) */
+        if (st == HONU_OK && (meta[i].present & HONU_ACL_SIZED)) {
+            const uint64_t actual = acl_list_bytes(&meta[i], acl);
+            if (actual != meta[i].acl_bytes) {
+                sz = sz - actual + meta[i].acl_bytes;
+                st = -HONU_ERR_INPUT; /* (marks the record for the encode pass) */
+            }
+        }
         out_off[i] = pos;
         pos += sz;
         if (status) status[i] = st;
     }
     out_off[n] = pos;
     for (uint64_t i = 0; i < n; i++) {
+        if (status && status[i] == -HONU_ERR_INPUT) {
+            status[i] = out_off[i + 1] > out_cap ? HONU_ERR_CAPACITY : HONU_ERR_INPUT;
+            continue;
+        }
         if (status && status[i] != HONU_OK) continue;
         uint64_t beg = out_off[i], end = out_off[i + 1];
         if (end > out_cap) {
@@ -597,7 +636,7 @@ int oracle_marshal_batch(const honu_meta *meta, const uint8_t *var, uint64_t var
 int oracle_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint64_t n, honu_meta *meta,
                         honu_record_info *info, honu_acl *acl, uint64_t acl_cap,
                         uint32_t *regions, uint64_t regions_cap, uint8_t *data, uint64_t data_cap,
-                        uint64_t totals[3], int acl_inplace) {
+                        uint64_t totals[3], int forms) {
     uint64_t acl_pos = 0, reg_pos = 0, data_pos = 0;
     int any_cap = 0;
     for (uint64_t i = 0; i < n; i++) {
@@ -608,10 +647,10 @@ int oracle_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
         uint64_t acap = acl && acl_pos < acl_cap ? acl_cap - acl_pos : 0;
         uint64_t rcap = regions && reg_pos < regions_cap ? regions_cap - reg_pos : 0;
         oracle_decode(rec + beg, len, beg, &meta[i], &info[i], ao, acap, ro, rcap, &an, &rn,
-                      acl_inplace);
+                      forms);
         if (info[i].meta_status == HONU_OK) {
             if (an) meta[i].acl_off = acl_pos;
-            if (meta[i].regions_count) meta[i].regions_off = reg_pos;
+            if (rn) meta[i].regions_off = reg_pos;  /* (a list in place keeps its own) */
             if (acl_pos + an > acl_cap || reg_pos + rn > regions_cap) {
                 info[i].meta_status = HONU_ERR_CAPACITY;
                 any_cap = 1;

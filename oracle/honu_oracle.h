@@ -55,19 +55,27 @@ int oracle_marshal(const honu_meta *m, const uint8_t *var, uint64_t var_len, con
                    const uint8_t *data, uint64_t data_len, uint8_t *out, uint64_t cap,
                    uint64_t *out_len);
 
+/* Decode output forms (bits of `forms` below), the product's context params
+ * "acl_inplace" and "regions_inplace" (include/honu_codec.h). */
+#define ORACLE_ACL_INPLACE 1
+#define ORACLE_REGIONS_INPLACE 2
+
 /* Object.Metadata() + Object.Data() + Tombstone() + StorageVersion()
  * (object.go:47-134) of one record `o` of length len, located at absolute
  * offset `base` of its arena (spans and data_off are reported absolute).
  * ACL entries / regions are appended to acl_out / regions_out (capacities
  * given); *acl_n / *regions_n receive the counts decoded. On a Metadata error
- * the row is zeroed (Go returns nil, err) and counts are 0. acl_inplace != 0:
- * an ACL list whose entries are all present is returned in place, as the
- * product does by default (include/honu_codec.h HONU_ACL_INPLACE): acl_off is
- * the absolute offset of its first entry and nothing goes to acl_out. */
+ * the row is zeroed (Go returns nil, err) and counts are 0. forms &
+ * ORACLE_ACL_INPLACE: an ACL list whose entries are all present is returned in
+ * place, as the product does by default (include/honu_codec.h
+ * HONU_ACL_INPLACE): acl_off is the absolute offset of its first entry and
+ * nothing goes to acl_out. forms & ORACLE_REGIONS_INPLACE: a non-empty region
+ * list likewise (HONU_REGIONS_INPLACE, regions_off absolute, every uvarint
+ * still decoded with DecodeUint32's checks). */
 void oracle_decode(const uint8_t *o, uint64_t len, uint64_t base, honu_meta *m,
                    honu_record_info *info, honu_acl *acl_out, uint64_t acl_cap,
                    uint32_t *regions_out, uint64_t regions_cap, uint64_t *acl_n,
-                   uint64_t *regions_n, int acl_inplace);
+                   uint64_t *regions_n, int forms);
 
 /* Batch drivers with the same output conventions as the HIP path
  * (honu_marshal_batch / honu_decode_batch): sequential offsets == exclusive
@@ -82,7 +90,7 @@ int oracle_marshal_batch(const honu_meta *meta, const uint8_t *var, uint64_t var
 int oracle_decode_batch(const uint8_t *rec, const uint64_t *rec_off, uint64_t n, honu_meta *meta,
                         honu_record_info *info, honu_acl *acl, uint64_t acl_cap,
                         uint32_t *regions, uint64_t regions_cap, uint8_t *data, uint64_t data_cap,
-                        uint64_t totals[3], int acl_inplace);
+                        uint64_t totals[3], int forms);
 
 /* keys.New(oid, &Version.Scalar) (keys/keys.go:42-51) for a decoded row. */
 int oracle_key(const honu_meta *m, int32_t meta_status, uint8_t key[29]);

@@ -107,13 +107,21 @@ def marshal_batch(hb):
     return out[:total], out_off, status
 
 
+def forms(acl_inplace: bool = True, regions_inplace: bool = True) -> int:
+    """The oracle's `forms` bits (honu_oracle.h ORACLE_*_INPLACE)."""
+    return (1 if acl_inplace else 0) | (2 if regions_inplace else 0)
+
+
 def decode_batch(rec: np.ndarray, rec_off: np.ndarray, materialize: bool = False,
-                 acl_inplace: bool = True):
+                 acl_inplace: bool = True, regions_inplace: bool = True):
     """(meta rows, info, acl table, region table, data arena | None, totals[3]).
 
     acl_inplace (the product's default, context param "acl_inplace"): an ACL
     list whose entries are all present comes back in place (HONU_ACL_INPLACE,
-    acl_off absolute in `rec`), only lists with a nil entry in the table."""
+    acl_off absolute in `rec`), only lists with a nil entry in the table.
+    regions_inplace (the default, context param "regions_inplace"): every
+    non-empty region list comes back in place (HONU_REGIONS_INPLACE,
+    regions_off absolute in `rec`), the region table stays empty."""
     from honu_amd.metadata import ACL_DTYPE, INFO_DTYPE, META_DTYPE
     lib = load()
     n = len(rec_off) - 1
@@ -130,7 +138,7 @@ def decode_batch(rec: np.ndarray, rec_off: np.ndarray, materialize: bool = False
     totals = np.zeros(3, np.uint64)
     lib.oracle_decode_batch(_p(rec), _p(rec_off), n, _p(meta), _p(info), _p(acl), len(acl),
                             _p(reg), len(reg), _p(data), 0 if data is None else len(data),
-                            _p(totals), 1 if acl_inplace else 0)
+                            _p(totals), forms(acl_inplace, regions_inplace))
     return (meta[:n], info[:n], acl[: int(totals[0])], reg[: int(totals[1])],
             None if data is None else data[: int(totals[2])], totals)
 
@@ -177,7 +185,7 @@ class CycleWorkspace:
         self.lib.oracle_decode_batch(_p(self.out), _p(self.out_off), self.n, _p(self.meta),
                                      _p(self.info), _p(self.acl), len(self.acl), _p(self.reg),
                                      len(self.reg), _p(self.data), len(self.data), _p(self.totals),
-                                     1)  # the product's default ACL form (in place)
+                                     forms())  # the product's default forms (lists in place)
         return self.total
 
 

@@ -7,10 +7,14 @@ give for it, as raw little-endian files plus a SHA-256 manifest:
   <name>.records.bin / .offsets.bin   encoded records (CSR, u64 offsets)
   <name>.rows.bin / .info.bin         decoded honu_meta rows / honu_record_info
   <name>.acl.bin / .regions.bin       decoded ACL / region tables
-    (the default form: ACL lists with every entry present returned in place,
-    HONU_ACL_INPLACE; only lists with a nil entry in the ACL table)
-  <name>.rows_table.bin / .acl_table.bin   the same rows / ACL table with every
-    list in the table (context param acl_inplace 0)
+    (the default forms: ACL lists with every entry present returned in place,
+    HONU_ACL_INPLACE, and every region list in place, HONU_REGIONS_INPLACE;
+    only lists with a nil ACL entry in a table)
+  <name>.rows_table.bin / .acl_table.bin / .regions_table.bin   the same rows
+    and tables with every list in its table (context params acl_inplace 0,
+    regions_inplace 0)
+  totals (manifest): ACL entries, regions, data bytes of the default forms,
+    then the table forms' ACL entries and regions
 Encode fixtures regenerate their input from the seeded generator (or
 tests/fixtures.py:extreme_metas); decode fixtures carry malformed records.
 
@@ -93,13 +97,15 @@ def outputs(name):
         assert (st == 0).all()
     else:
         rec, off = malformed_records()
-    meta, info, acl, reg, _, tot = oracle.decode_batch(rec, off, False, acl_inplace=True)
-    tmeta, tinfo, tacl, treg, _, ttot = oracle.decode_batch(rec, off, False, acl_inplace=False)
-    assert tinfo.tobytes() == info.tobytes() and treg.tobytes() == reg.tobytes()
+    meta, info, acl, reg, _, tot = oracle.decode_batch(rec, off, False)
+    tmeta, tinfo, tacl, treg, _, ttot = oracle.decode_batch(rec, off, False, acl_inplace=False,
+                                                            regions_inplace=False)
+    assert tinfo.tobytes() == info.tobytes() and len(reg) == 0
     return {"records": rec.tobytes(), "offsets": off.astype("<u8").tobytes(),
             "rows": meta.tobytes(), "info": info.tobytes(), "acl": acl.tobytes(),
             "regions": reg.astype("<u4").tobytes(), "rows_table": tmeta.tobytes(),
-            "acl_table": tacl.tobytes()}, [int(x) for x in tot] + [int(ttot[0])]
+            "acl_table": tacl.tobytes(), "regions_table": treg.astype("<u4").tobytes()}, \
+        [int(x) for x in tot] + [int(ttot[0]), int(ttot[1])]
 
 
 NAMES = list(ENCODE) + ["malformed"]

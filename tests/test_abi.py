@@ -50,7 +50,7 @@ STRUCTS = ((META_DTYPE, "honu_meta"), (ACL_DTYPE, "honu_acl"), (INFO_DTYPE, "hon
 
 def test_abi_self_description():
     lib = _lib.load()
-    assert lib.honu_abi_version() == 5
+    assert lib.honu_abi_version() == 6
     assert lib.honu_sizeof_meta() == META_DTYPE.itemsize == 352
     assert lib.honu_sizeof_acl() == ACL_DTYPE.itemsize == 20
     assert lib.honu_sizeof_record_info() == INFO_DTYPE.itemsize == 32
@@ -75,6 +75,25 @@ def test_struct_offsets_match_numpy(tmp_path):
     for dt, ct in STRUCTS:
         for name in dt.names:
             assert int(got[f"{ct}.{name}"]) == dt.fields[name][1], (ct, name)
+
+
+def test_product_library_reads_no_environment():
+    """The product library behaves the same whatever the caller's process
+    environment holds: it imports no getenv at all, so
+    HONU_ACL_INPLACE=0 and the like cannot change its outputs; only the A/B
+    build (make ab) reads HONU_* variables. (tests/test_gpu_parity.py
+    test_environment_is_ignored checks the same on the GPU.)"""
+    if _lib.LIB_PATH != os.path.join(ROOT, "honu_amd", "libhonu_codec.so"):
+        pytest.skip("HONU_LIB_PATH points at another build")
+    out = subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], check=True,
+                         capture_output=True, text=True).stdout
+    imported = {ln.split()[-1].split("@")[0] for ln in out.splitlines() if ln.strip()}
+    assert not imported & {"getenv", "secure_getenv", "__secure_getenv"}, imported & {"getenv"}
+    ab = os.path.join(ROOT, "honu_amd", "libhonu_codec_ab.so")
+    if os.path.exists(ab):  # the measurement build does read them
+        out = subprocess.run(["nm", "-D", "--undefined-only", ab], check=True, capture_output=True,
+                             text=True).stdout
+        assert "getenv" in out
 
 
 def test_no_gpu_fails_loudly():

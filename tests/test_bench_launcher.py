@@ -51,12 +51,14 @@ def test_world_size_must_match():
 
 
 def test_default_line_legs():
-    """--legs: the default 1M Large encdec line carries configs[1] (small) and
-    configs[3] (mixed_encode); other lines none unless asked; 'none' and
-    unknown legs (no GPU needed: argument handling only)."""
+    """--legs: the default 1M Large encdec line carries configs[1] (small),
+    configs[3] (mixed_encode) and the README's Medium and XLarge shapes
+    (north_star: all four shapes on the driver's line); other lines none
+    unless asked; 'none' and unknown legs (no GPU needed: argument handling
+    only)."""
     sys.path.insert(0, ROOT)
     import bench
-    assert bench.legs_of(bench.parse_args([])) == ["small", "mixed_encode"]
+    assert bench.legs_of(bench.parse_args([])) == ["small", "mixed_encode", "medium", "xlarge"]
     assert bench.legs_of(bench.parse_args(["--legs", "none"])) == []
     assert bench.legs_of(bench.parse_args(["--shape", "small"])) == []
     assert bench.legs_of(bench.parse_args(["--records", "1000"])) == []
@@ -64,5 +66,7 @@ def test_default_line_legs():
     assert bench.legs_of(bench.parse_args(["--shape", "medium", "--legs", "small"])) == ["small"]
     with pytest.raises(SystemExit):
         bench.legs_of(bench.parse_args(["--legs", "small,bogus"]))
-    # the legs' configurations: Small encode + decode, Mixed encode only
-    assert bench.LEG_SHAPES == {"small": ("small", False), "mixed_encode": ("mixed", True)}
+    # the legs' configurations: Small / Medium encode + decode, Mixed encode
+    # only, XLarge encode + decode of 1/16 the records (64 K) + its zero copy
+    assert bench.LEG_SHAPES == {"small": ("small", False, 1, False), "mixed_encode": ("mixed", True, 1, False),
+                                "medium": ("medium", False, 1, False), "xlarge": ("xlarge", False, 1 / 16, True)}

@@ -163,7 +163,8 @@ def test_bench_encode_only_bit_exact(oracle_lib, shape, n):
 def test_bench_verify_detects_corruption():
     """_verify_chunk (honu_verify_decoded + digests) flags one wrong byte in a
     decoded ObjectID, span, ACL entry (in place in the records arena: its
-    flag, a ClientID byte, its Permissions; or in the table), region or
+    flag, a ClientID byte, its Permissions; or in the table), region (in
+    place: a byte of its uvarint in the records arena; or in the table) or
     payload."""
     args = bench.parse_args(["--records", "600", "--shape", "small", "--min-chunks", "1"])
     b = bench.Bench(args, 0, 0)
@@ -195,8 +196,16 @@ def test_bench_verify_detects_corruption():
     assert nacl and pr & ACL_INPLACE and int(tot[0]) == 0  # the generator writes no nil entry
     for k in (0, 1, 17):  # the 2nd entry's flag, a ClientID byte, the Permissions byte
         assert not flip(sl.out, acl_off + 18 * (nacl // 2) + k)
-    for x in b.slots:  # the table form
+    from honu_amd.metadata import REGIONS_INPLACE
+    nreg = rows[:, 344:352].copy().view(np.uint64)[:, 0]
+    j = int(np.flatnonzero(nreg > 1)[0])
+    pr = int(rows[j, 0:4].view(np.uint32)[0])
+    assert pr & REGIONS_INPLACE and int(tot[1]) == 0  # every region list in place
+    reg_off = int(rows[j, 336:344].view(np.uint64)[0])
+    assert not flip(sl.out, reg_off)                 # the first region's uvarint
+    for x in b.slots:  # the table forms
         _lib.check(b.lib.honu_ctx_set_param(x.codec.ctx, b"acl_inplace", 0), "param")
+        _lib.check(b.lib.honu_ctx_set_param(x.codec.ctx, b"regions_inplace", 0), "param")
     sl = b._issue(a, z, False)
     torch.cuda.synchronize()
     assert b._verify_chunk(a, z, sl)

@@ -35,22 +35,30 @@ def test_c_demo_marshal_decode(shape, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("form", ["inplace", "table"])
 @pytest.mark.parametrize("shape,n", [(2, 512), (0, 20000)], ids=["large", "small"])
-def test_c_demo_count_sized_tables_vs_oracle(tmp_path, oracle_lib, shape, n):
+def test_c_demo_count_sized_tables_vs_oracle(tmp_path, oracle_lib, shape, n, form):
     """The binding's DecodeBatch flow: ACL / region tables
     sized by the batch's entry counts through the retry on the totals the
-    first call reports (its caps are one entry per record, so the retry always
-    runs), not by record bytes. Everything the zero-copy decode returned is
-    bit-exact with the oracle's decode of the same records, and the tables
-    take their exact entry counts: a small fraction of the records arena."""
+    first call reports, not by record bytes. Table forms (acl_inplace 0,
+    regions_inplace 0): the first call's caps are one entry per record, so the
+    retry always runs. In-place forms (the defaults): the generator's lists
+    need no table entry, so one call with empty tables is enough, and the
+    demo rebuilds every ACL entry and region from the records arena.
+    Everything the zero-copy decode returned is bit-exact with the oracle's
+    decode of the same records, and the tables take their exact entry
+    counts: a small fraction of the records arena (nothing in place)."""
     import numpy as np
     from honu_amd.metadata import ACL_DTYPE, INFO_DTYPE, META_DTYPE
-    r = subprocess.run([DEMO, str(shape), str(n), str(tmp_path)], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([DEMO, str(shape), str(n), str(tmp_path), form], capture_output=True, text=True,
+                       timeout=300)
     assert r.returncode == 0, r.stderr
-    assert "decode calls 2," in r.stdout
+    assert ("decode calls 2," if form == "table" else "decode calls 1,") in r.stdout
     rd = lambda name, dt: np.fromfile(tmp_path / name, dtype=dt)  # noqa: E731
     rec, off = rd("rec.bin", np.uint8), rd("off.bin", np.uint64)
-    ometa, oinfo, oacl, oreg, _, otot = oracle_lib.decode_batch(rec, off, False)
+    inpl = form == "inplace"
+    ometa, oinfo, oacl, oreg, _, otot = oracle_lib.decode_batch(rec, off, False, inpl, inpl)
+    assert inpl == (int(otot[0]) + int(otot[1]) == 0)
     assert np.array_equal(rd("tot.bin", np.uint64), otot)
     assert rd("meta.bin", META_DTYPE).tobytes() == ometa.tobytes()
     assert rd("info.bin", INFO_DTYPE).tobytes() == oinfo.tobytes()

@@ -55,18 +55,20 @@ def test_gpu_reproduces_fixture(name):
             assert out.tobytes() == rec.tobytes()
         d_rec = hobj._dev_bytes(rec if len(rec) else np.zeros(1, np.uint8), c.torch_device)
         d_off = hobj._dev_bytes(off, c.torch_device)
-        # both ACL forms (totals: ACL, regions, data bytes, then the table
-        # form's ACL entries), both decodes (single launch, split)
-        for inplace, rows, acls in ((1, "rows", "acl"), (0, "rows_table", "acl_table")):
+        # both list forms (totals: ACL, regions, data bytes of the in-place
+        # forms, then the table forms' ACL entries and regions), both decodes
+        # (single launch, split)
+        for inplace, sfx in ((1, ""), (0, "_table")):
             hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"acl_inplace", inplace), "param")
+            hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"regions_inplace", inplace), "param")
             for rv in (6, 5):
                 hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", rv), "param")
                 meta, info, acl, reg, _, tot = c.decode(d_rec, d_off, n, rec_bytes=int(off[-1])).host()
                 want = MANIFEST[name]["totals"]
-                assert [int(x) for x in tot] == (want[:3] if inplace else [want[3]] + want[1:3])
-                assert meta.tobytes() == np.frombuffer(_file(name, rows), META_DTYPE).tobytes()
+                assert [int(x) for x in tot] == (want[:3] if inplace else [want[3], want[4], want[2]])
+                assert meta.tobytes() == np.frombuffer(_file(name, "rows" + sfx), META_DTYPE).tobytes()
                 assert info.tobytes() == np.frombuffer(_file(name, "info"), INFO_DTYPE).tobytes()
-                assert acl.tobytes() == np.frombuffer(_file(name, acls), ACL_DTYPE).tobytes()
-                assert reg.tobytes() == _file(name, "regions")
+                assert acl.tobytes() == np.frombuffer(_file(name, "acl" + sfx), ACL_DTYPE).tobytes()
+                assert reg.tobytes() == _file(name, "regions" + sfx)
     finally:
         c.close()

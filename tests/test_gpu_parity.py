@@ -23,14 +23,18 @@ from honu_amd.metadata import META_DTYPE, normalize, pack_batch, unpack_row  # n
 from honu_amd.workload import gen_host_batch, gen_meta  # noqa: E402
 
 
-@pytest.fixture(scope="module", params=[(6, 2, 1), (5, 0, 1), (6, 1, 1), (6, 2, 0), (5, 2, 0)],
-                ids=["fused", "split", "fork", "fused_table", "split_table"])
+@pytest.fixture(scope="module", params=[(6, 2, 1, 1), (5, 0, 1, 1), (6, 1, 1, 1), (6, 2, 0, 0), (5, 2, 0, 0),
+                                        (6, 2, 1, 0), (5, 2, 0, 1)],
+                ids=["fused", "split", "fork", "fused_table", "split_table", "fused_regtable",
+                     "split_acltable"])
 def codec(request):
-    """Both metadata decodes of the product library with both ACL forms, and
+    """Both metadata decodes of the product library with both list forms, and
     both placements of the encoder's ACL lists: the single-launch decode
     (fused.hip) at every batch size and the split decode kernels (windowed
-    lane parse, group fill); ACL lists returned in place (acl_inplace 1, the
-    default) or every list in the ACL table ("_table"). The default picks the
+    lane parse, group fill); ACL and region lists returned in place
+    (acl_inplace 1 and regions_inplace 1, the defaults) or every list in the
+    ACL and region tables ("_table"), or one list kind in its table
+    ("_regtable": the round-5 default, "_acltable"). The default picks the
     decode by batch size; the bench pipeline and large-batch tests run it.
     The encoder is the lane encoder + group ACL lists (lane.hip, grp.hip):
     "split" runs the lists' kernel after the lane encoder (encode_fork 0),
@@ -40,11 +44,13 @@ def codec(request):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     c = hobj.Codec(0, 1 << 18)
-    rv, fork, inplace = request.param
+    rv, fork, inplace, reg_inplace = request.param
     hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", rv), "param")
     hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"encode_fork", fork), "param")
     hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"acl_inplace", inplace), "param")
+    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"regions_inplace", reg_inplace), "param")
     c.acl_inplace = bool(inplace)
+    c.regions_inplace = bool(reg_inplace)
     yield c
     c.close()
 
@@ -70,7 +76,7 @@ def gpu_decode(codec, rec, off, materialize=False):
 def assert_decode_equal(oracle_lib, codec, rec, off, materialize=False):
     meta, info, acl, reg, data, tot = gpu_decode(codec, rec, off, materialize)
     ometa, oinfo, oacl, oreg, odata, otot = oracle_lib.decode_batch(
-        rec, off, materialize, getattr(codec, "acl_inplace", True))
+        rec, off, materialize, getattr(codec, "acl_inplace", True), getattr(codec, "regions_inplace", True))
     n = len(off) - 1
     assert np.array_equal(tot, otot)
     assert info.tobytes() == oinfo.tobytes()
@@ -172,14 +178,34 @@ def test_keys_parity(codec, oracle_lib):
 
 
 def test_encode_input_errors(codec, oracle_lib):
+    """Rows the encoder refuses (HONU_ERR_INPUT / PANIC), as the oracle: a
+    span or list outside its arena, and a carried ACL list length
+    (HONU_ACL_SIZED) outside [count, 18 count] (the size
+    pass) or inside it but not the list's length (the list kernel, which reads
+    every entry: the record keeps the range its carried length sized and
+    reports HONU_ERR_INPUT; its bytes are unspecified). A row without the bit
+    is sized from the table as before."""
+    from honu_amd.metadata import ACL_SIZED
     meta, data = load_object_fixture()
-    hb = pack_batch([meta, None, meta, meta], [data, b"a", b"", data])
+    hb = pack_batch([meta, None, meta, meta, meta, meta, meta, meta],
+                    [data, b"a", b"", data, data, b"zz", data, b""])
+    assert int(hb.meta[0]["present"]) & ACL_SIZED and int(hb.meta[0]["acl_bytes"]) == 36
     hb.meta[2]["mime"]["off"] = 10**9          # span outside the var arena
     hb.meta[3]["acl_count"] = 10**6            # list outside the ACL table
+    hb.meta[4]["acl_bytes"] = 19               # a lying length: 2 entries, not 1 present + 1 nil
+    hb.meta[5]["acl_bytes"] = 37               # outside [2, 36]
+    hb.meta[6]["present"] = int(hb.meta[6]["present"]) & ~ACL_SIZED  # no carried length: the table is read
+    hb.meta[7]["acl_bytes"] = 1                # below the count
     out, off, st = gpu_marshal(codec, hb)
     oout, ooff, ost = oracle_lib.marshal_batch(hb)
-    assert st.tolist() == ost.tolist() == [0, 8, 10, 10]
-    assert np.array_equal(off, ooff) and out.tobytes() == oout.tobytes()
+    assert st.tolist() == ost.tolist() == [0, 8, 10, 10, 10, 10, 0, 10]
+    assert np.array_equal(off, ooff)
+    lie = slice(int(off[4]), int(off[5]))
+    assert lie.stop - lie.start == int(off[1]) - int(off[0]) - 17  # sized by 19 bytes, not 36
+    g, o = out.copy(), oout.copy()
+    g[lie] = 0
+    o[lie] = 0
+    assert g.tobytes() == o.tobytes()
 
 
 def test_decode_capacity(codec, oracle_lib):
@@ -192,8 +218,13 @@ def test_decode_capacity(codec, oracle_lib):
     meta, info, acl, reg, data, tot = d.host()
     # the generator writes no nil ACL entry: in place, no list needs the table
     assert (int(tot[0]) == 0 if codec.acl_inplace else int(tot[0]) > 10) and int(tot[2]) > 4096
-    assert int(tot[1]) > 10
-    assert (info["meta_status"] == 9).any() and (info["data_status"] == 9).any()
+    assert int(tot[1]) == 0 if codec.regions_inplace else int(tot[1]) > 10
+    # (lists in place take no table entry: no record fails the small caps)
+    if codec.acl_inplace and codec.regions_inplace:
+        assert (info["meta_status"] == 0).all()
+    else:
+        assert (info["meta_status"] == 9).any()
+    assert (info["data_status"] == 9).any()
     ok = info["data_status"] == 0
     assert (info["data_off"][ok] + info["data_len"][ok] <= 4096).all()
 
@@ -489,7 +520,8 @@ def test_decode_parse_full_waves(codec, oracle_lib):
     hb = gen_host_batch(23, "small", 0, n)
     rec, off, _ = oracle_lib.marshal_batch(hb)
     meta, info, acl, reg, data, tot = gpu_decode(codec, rec, off)
-    ometa, oinfo, oacl, oreg, odata, otot = oracle_lib.decode_batch(rec, off, False, codec.acl_inplace)
+    ometa, oinfo, oacl, oreg, odata, otot = oracle_lib.decode_batch(rec, off, False, codec.acl_inplace,
+                                                                    codec.regions_inplace)
     assert np.array_equal(tot, otot) and info.tobytes() == oinfo.tobytes()
     assert meta.tobytes() == ometa.tobytes()
     assert acl.tobytes() == oacl.tobytes() and reg.tobytes() == oreg.tobytes()
@@ -681,3 +713,137 @@ def test_hbm_probe_modes(codec):
         torch.cuda.synchronize()
         assert int((b.view(torch.int32)[2::4] == 1).sum()) == nbytes // 16
     assert codec.lib.honu_hbm_probe(codec.ctx, 7, None, None, 16, 1, codec.stream) != 0
+
+
+def test_environment_is_ignored(oracle_lib, monkeypatch):
+    """The product library takes its configuration from honu_ctx_set_param
+    only: HONU_* variables set in the process before the
+    context is created change neither its parameters nor its outputs (the ACL
+    lists still come back in place with HONU_ACL_INPLACE=0). The A/B build
+    reads them (HONU_LIB_PATH set: skipped)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import os
+    if os.environ.get("HONU_LIB_PATH"):
+        pytest.skip("A/B build")
+    env = {"HONU_ACL_INPLACE": "0", "HONU_RECORD_VARIANT": "5", "HONU_LANE_BLOCKS": "3",
+           "HONU_COPY_BLOCKS": "1", "HONU_ENCODE_FORK": "0", "HONU_GUARD_BLOCKS": "7",
+           "HONU_INLINE_RECOVERY": "1", "HONU_RECORD_BLOCKS": "1"}
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    c = hobj.Codec(0, 4096)
+    try:
+        got = {}
+        for name in ("acl_inplace", "record_variant", "lane_blocks", "encode_fork", "guard_blocks",
+                     "inline_recovery"):
+            v = ctypes.c_int64(-1)
+            hobj._lib.check(c.lib.honu_ctx_get_param(c.ctx, name.encode(), ctypes.byref(v)), "param")
+            got[name] = v.value
+        assert got == {"acl_inplace": 1, "record_variant": 0, "lane_blocks": 0, "encode_fork": 2,
+                       "guard_blocks": 0, "inline_recovery": 0}
+        hb = gen_host_batch(71, "small", 0, 300)
+        rec, off, _ = oracle_lib.marshal_batch(hb)
+        meta, info, acl, reg, data, tot = gpu_decode(c, rec, off)
+        ometa, oinfo, oacl, oreg, _, otot = oracle_lib.decode_batch(rec, off, False)
+        assert meta.tobytes() == ometa.tobytes() and np.array_equal(tot, otot)
+        assert (meta["present"] & (1 << 8)).any()  # HONU_ACL_INPLACE
+    finally:
+        c.close()
+
+
+def test_copy_counter_lines_concurrent(oracle_lib):
+    """The range tails' counters (copy.hip): payload copies of one
+    context issued back to back on two streams at once, each into its own
+    records arena, with payloads averaging >= 16 KB so every launch takes
+    tails from a counter. Every copy call counts on a line of its own, so no
+    launch skips a tail another took: every arena bit-exact."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    L = hobj._lib
+    n = 1500
+    rng = np.random.default_rng(19)
+    base = gen_host_batch(19, "small", 0, n)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(rng.integers(16 << 10, 60 << 10, n))
+    pay = rng.integers(0, 256, int(off[-1]) + 1, dtype=np.uint8)
+    from honu_amd.metadata import HostBatch
+    hb = HostBatch(base.meta, base.var, base.acl, base.regions, pay, off)
+    oout, ooff, _ = oracle_lib.marshal_batch(hb)
+    total = int(ooff[-1])
+    c = hobj.Codec(0, n)
+    try:
+        db = hobj.DeviceBatch.from_host(hb, c.torch_device)
+        out_off, status = c._empty(8 * (n + 1)), c._empty(4 * n)
+        c.encode_sizes(db, out_off, status)
+        c.scan(out_off, n, out_off)
+        outs = [c._empty(total) for _ in range(8)]
+        for o in outs:  # headers and tails (plain form), then only the copies race
+            L.check(c.lib.honu_encode_records(c.ctx, L.ptr(db.meta), L.ptr(db.var), L.ptr(db.acl),
+                                              L.ptr(db.regions), L.ptr(db.payload_off), n, L.ptr(o),
+                                              total, L.ptr(out_off), L.ptr(status), c.stream), "records")
+        torch.cuda.synchronize()
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        for rep in range(3):
+            for k, o in enumerate(outs):
+                s = streams[k % 2]
+                L.check(c.lib.honu_encode_payloads(c.ctx, L.ptr(db.payload), L.ptr(db.payload_off), n,
+                                                   L.ptr(o), total, L.ptr(out_off), L.ptr(status),
+                                                   s.cuda_stream), "payloads")
+        torch.cuda.synchronize()
+        for o in outs:
+            assert hobj._to_host(o, total, np.uint8).tobytes() == oout.tobytes()
+    finally:
+        c.close()
+
+
+def test_encode_forms_not_mixed_and_null_payload(oracle_lib):
+    """The payload-unit pair and the plain pair complete different bytes
+    (honu_codec.h): a payload call of the other form than the context's last
+    records call is refused (HONU_E_ARG) instead of leaving bytes unwritten
+    with every status OK. honu_encode of a batch whose payloads are all empty
+    accepts a null payload arena."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    L = hobj._lib
+    n = 200
+    hb = gen_host_batch(29, "small", 0, n)
+    oout, ooff, _ = oracle_lib.marshal_batch(hb)
+    total = int(ooff[-1])
+    c = hobj.Codec(0, n)
+    try:
+        db = hobj.DeviceBatch.from_host(hb, c.torch_device)
+        out_off, status, out = c._empty(8 * (n + 1)), c._empty(4 * n), c._empty(total)
+        c.encode_sizes(db, out_off, status)
+        c.scan(out_off, n, out_off)
+        args = (c.ctx, L.ptr(db.meta), L.ptr(db.var), L.ptr(db.acl), L.ptr(db.regions))
+        L.check(c.lib.honu_encode_records(*args, L.ptr(db.payload_off), n, L.ptr(out), total,
+                                          L.ptr(out_off), L.ptr(status), c.stream), "records")
+        assert c.lib.honu_encode_payloads_units(c.ctx, L.ptr(db.payload), L.ptr(db.payload_off), n,
+                                                L.ptr(out), total, L.ptr(out_off), L.ptr(status),
+                                                c.stream) == -1
+        L.check(c.lib.honu_encode_payloads(c.ctx, L.ptr(db.payload), L.ptr(db.payload_off), n, L.ptr(out),
+                                           total, L.ptr(out_off), L.ptr(status), c.stream), "payloads")
+        torch.cuda.synchronize()
+        assert hobj._to_host(out, total, np.uint8).tobytes() == oout.tobytes()
+        L.check(c.lib.honu_encode_records_units(*args, L.ptr(db.payload), L.ptr(db.payload_off), n,
+                                                L.ptr(out), total, L.ptr(out_off), L.ptr(status),
+                                                c.stream), "records_units")
+        assert c.lib.honu_encode_payloads(c.ctx, L.ptr(db.payload), L.ptr(db.payload_off), n, L.ptr(out),
+                                          total, L.ptr(out_off), L.ptr(status), c.stream) == -1
+        # every payload empty (tombstones): a null payload arena is accepted
+        from honu_amd.metadata import HostBatch
+        eoff = np.zeros(n + 1, np.uint64)
+        eb = HostBatch(hb.meta, hb.var, hb.acl, hb.regions, np.zeros(1, np.uint8), eoff)
+        eout, eooff, _ = oracle_lib.marshal_batch(eb)
+        etotal = int(eooff[-1])
+        edb = hobj.DeviceBatch.from_host(eb, c.torch_device)
+        eo, est, eoo = c._empty(etotal), c._empty(4 * n), c._empty(8 * (n + 1))
+        L.check(c.lib.honu_marshal_batch(c.ctx, L.ptr(edb.meta), L.ptr(edb.var), edb.var_len,
+                                         L.ptr(edb.acl), edb.acl_len, L.ptr(edb.regions), edb.regions_len,
+                                         None, L.ptr(edb.payload_off), n, L.ptr(eo), etotal, L.ptr(eoo),
+                                         L.ptr(est), c.stream), "marshal null payload")
+        torch.cuda.synchronize()
+        assert (hobj._to_host(est, 4 * n, np.int32) == 0).all()
+        assert hobj._to_host(eo, etotal, np.uint8).tobytes() == eout.tobytes()
+    finally:
+        c.close()

@@ -15,10 +15,12 @@ the scans' form). Both tile modes advance the same epoch: a test alternates
 them, across an epoch wrap reached by static launches. Then the speculative
 launches' recovery (late-failing records, nil ACL entries, a long unstaged list
 under a capacity failure) and concurrent launches on two streams. The
-speculation and tile tests run with both ACL forms (context param
-acl_inplace: lists with every entry present returned in place, the default,
-whose speculated flags the launch gathers after its publish; or every list in
-the table, whose flags the table fill checks)."""
+speculation and tile tests run with three list forms (context params
+acl_inplace and regions_inplace): both kinds of list in place, the default
+(ACL lists whose speculated flags the launch gathers after its publish; tiles
+with no table entry skip the look-back wait); every list in its table (ACL
+flags checked by the table fill); and ACL lists in place with the regions in
+their table (the round-5 default: every tile waits for its region offsets)."""
 import numpy as np
 import pytest
 
@@ -30,11 +32,20 @@ from honu_amd import object as hobj  # noqa: E402
 from honu_amd.workload import gen_host_batch  # noqa: E402
 
 EPOCHS = 1 << 18
-FORMS = pytest.mark.parametrize("inplace", [1, 0], ids=["acl_inplace", "acl_table"])
+FORMS = pytest.mark.parametrize("inplace", [1, 0, 2], ids=["lists_inplace", "lists_table", "regions_table"])
+# form code -> (acl_inplace, regions_inplace)
+FORM_PARAMS = {1: (1, 1), 0: (0, 0), 2: (1, 0)}
 
 
 def _form(c, inplace):
-    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"acl_inplace", inplace), "param")
+    acl, reg = FORM_PARAMS[inplace]
+    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"acl_inplace", acl), "param")
+    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"regions_inplace", reg), "param")
+
+
+def _oracle(oracle_lib, rec, off, inplace, materialize=False):
+    acl, reg = FORM_PARAMS[inplace]
+    return oracle_lib.decode_batch(rec, off, materialize, bool(acl), bool(reg))
 
 
 def _dev(a, codec):
@@ -64,7 +75,7 @@ class _Dec:
 
     def check(self, oracle_lib, rec, off):
         torch.cuda.synchronize()
-        ometa, oinfo, oacl, oreg, _, otot = oracle_lib.decode_batch(rec, off, False, bool(self.inplace))
+        ometa, oinfo, oacl, oreg, _, otot = _oracle(oracle_lib, rec, off, self.inplace)
         tot = self.tot[:24].cpu().numpy().view(np.uint64)
         assert np.array_equal(tot, otot)
         assert self.meta[:352 * self.n].cpu().numpy().tobytes() == ometa.tobytes()
@@ -382,7 +393,7 @@ def test_speculated_long_list_checked_under_capacity_failure(oracle_lib, inplace
     assert r2[-7:].tobytes() == bytes(7)  # last region 0, then six zero bytes
     brec = np.concatenate([rec, r2])
     boff = np.concatenate([off, off[-1] + o2[1:]]).astype(np.uint64)
-    ometa, oinfo, oacl, oreg, _, otot = oracle_lib.decode_batch(brec, boff, False, bool(inplace))
+    ometa, oinfo, oacl, oreg, _, otot = _oracle(oracle_lib, brec, boff, inplace)
     assert int(ometa[-1]["regions_count"]) == 5 and int(ometa[-1]["acl_count"]) == 1200
     acl_cap, reg_cap = int(otot[0]) - 1, int(otot[1]) + 16
     c = hobj.Codec(0, n)
@@ -403,7 +414,8 @@ def test_speculated_long_list_checked_under_capacity_failure(oracle_lib, inplace
         assert d.info[:32 * n].cpu().numpy().tobytes() == bytes(want)
         nacl = int(otot[0]) - 1200  # the entries of every record before the last
         assert d.acl[:20 * nacl].cpu().numpy().tobytes() == oacl[:nacl].tobytes()
-        nreg = int(otot[1]) - 5  # the capacity-failed record stores no regions either
+        # the capacity-failed record stores no regions either (in place: none at all)
+        nreg = int(otot[1]) - (0 if FORM_PARAMS[inplace][1] else 5)
         assert d.reg[:4 * nreg].cpu().numpy().tobytes() == oreg[:nreg].tobytes()
     finally:
         c.close()

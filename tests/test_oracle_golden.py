@@ -8,8 +8,8 @@ import pytest
 
 from fixtures import (load_json, load_object_fixture, metadata_from_json, py_marshal, py_uvarint,
                       py_varint)
-from honu_amd.metadata import (HAS_META, Metadata, Scalar, Version, normalize, pack_batch,
-                               unpack_row)
+from honu_amd.metadata import (HAS_META, REGIONS_INPLACE, Metadata, Scalar, Version, normalize,
+                               pack_batch, unpack_row)
 
 
 def marshal(oracle_lib, meta, data):
@@ -242,8 +242,16 @@ def test_uint32_window(oracle_lib):
     base = b"\x01" + bytes(32) + b"\x00\x00\x00" + bytes(32) + b"\x07\x00"  # ... perms, ACL 0
     tail = b"\x00\x00\x00\x00" + b"\x2a" + b"\x00\x00"
     ok = _tail_record(base + b"\x01\xff\xff\xff\xff\x7f" + tail)
+    rec = np.frombuffer(ok, np.uint8)
+    off = np.array([0, len(ok)], np.uint64)
+    # the table form: the truncated value in the region table
+    m, info, acl, reg, _, _ = oracle_lib.decode_batch(rec, off, False, regions_inplace=False)
+    assert info[0]["meta_status"] == 0 and list(reg) == [0xFFFFFFFF]
+    # in place (the default): the 5-byte uvarint in the record, read back the same way
     m, info, acl, reg, *_ = decode(oracle_lib, ok)
-    assert info["meta_status"] == 0 and list(reg) == [0xFFFFFFFF]
+    assert info["meta_status"] == 0 and len(reg) == 0 and m["present"] & REGIONS_INPLACE
+    assert int(m["regions_off"]) == len(ok) - len(tail) - 5
+    assert unpack_row(m, rec).WriteRegions == [0xFFFFFFFF]
     bad = _tail_record(base + b"\x01\xff\xff\xff\xff\xff\x01" + tail)
     _, info, *_ = decode(oracle_lib, bad)
     assert info["meta_status"] == 7

@@ -32,7 +32,10 @@ def main():
     f = per_kernel(fetch_csv, "FETCH_SIZE")
     w = per_kernel(write_csv, "WRITE_SIZE")
     res = {"workload": workload, "source": [fetch_csv, write_csv],
-           "correction": "bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024", "kernels": {}}
+           "correction": "bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024",
+           # the commit the measured tree was (HONU_COMMIT, set by the caller:
+           # the GPU box has no .git), read back by bench.py (roofline.traffic_commit)
+           "commit": os.environ.get("HONU_COMMIT"), "kernels": {}}
     for k in sorted(set(f) | set(w)):
         fv, wv = f.get(k, []), w.get(k, [])
         fb = 2 * 1024 * sum(fv) / max(1, len(fv))
