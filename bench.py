@@ -137,6 +137,10 @@ def parse_args(argv=None):
     p.add_argument("--decode-leg", choices=["both", "zero_copy", "materialising"], default="both",
                    help="decode mode: run one leg only (PMC passes attribute a kernel's traffic "
                         "to one leg)")
+    p.add_argument("--zc-forms", choices=["all", "default"], default="all",
+                   help="decode legs: the zero-copy leg times the default list forms and, for "
+                        "comparison, the table forms and speculation off (all), or the default forms "
+                        "only (default: PMC passes, whose per-kernel averages would mix the forms)")
     p.add_argument("--no-host-path", action="store_true",
                    help="encdec mode: skip the host-path leg (PMC passes: its small launches "
                         "would mix into the copy kernels' per-launch averages)")
@@ -781,13 +785,15 @@ class DecodeBench:
         torch.cuda.synchronize()
         return [x.elapsed_time(y) for x, y in ev]
 
-    def _form_reps(self, acl, reg, reps):
+    def _form_reps(self, acl, reg, reps, speculate=1):
         """reps timed calls with the context params acl_inplace / regions_inplace
         set to (acl, reg): (per-call ms, ACL table entries, region table entries)."""
         c = self.codec.ctx
         _lib.check(self.lib.honu_ctx_set_param(c, b"acl_inplace", acl), "param")
         _lib.check(self.lib.honu_ctx_set_param(c, b"regions_inplace", reg), "param")
+        _lib.check(self.lib.honu_ctx_set_param(c, b"speculate", speculate), "param")
         ms = self._zero_copy_reps(reps)
+        _lib.check(self.lib.honu_ctx_set_param(c, b"speculate", 1), "param")
         tt = self.totals[:16].view(torch.int64).tolist()
         return ms, int(tt[0]), int(tt[1])
 
@@ -807,9 +813,12 @@ class DecodeBench:
         regions in their table (round 5's default). The forms alternate, the
         default's reps split around the others."""
         h = max(1, reps // 2)
+        others = getattr(self.args, "zc_forms", "all") == "all"
         ms = self._form_reps(1, 1, h)[0]
-        ms_tab, tab_acl, tab_reg = self._form_reps(0, 0, reps)
-        ms_r5, r5_acl, r5_reg = self._form_reps(1, 0, reps)
+        if others:
+            ms_tab, tab_acl, tab_reg = self._form_reps(0, 0, reps)
+            ms_r5, r5_acl, r5_reg = self._form_reps(1, 0, reps)
+            ms_ns, ns_acl, ns_reg = self._form_reps(1, 1, reps, speculate=0)
         ms2, acl_e, reg_e = self._form_reps(1, 1, reps - h)
         ms = ms + ms2
         t = sum(ms) / len(ms) / 1e3
@@ -826,10 +835,14 @@ class DecodeBench:
                            f"{acl_e} ACL and {reg_e} region table entries written"),
             "table_form": self._form_summary(
                 ms_tab, tab_acl, tab_reg, "the same call with acl_inplace 0 and regions_inplace 0: "
-                "every list copied into the 20-byte ACL and 4-byte region tables (rounds 1-4)"),
+                "every list copied into the 20-byte ACL and 4-byte region tables (rounds 1-4)")
+            if others else None,
             "regions_table_form": self._form_summary(
                 ms_r5, r5_acl, r5_reg, "the same call with regions_inplace 0: ACL lists in place, "
-                "region lists in their table (round 5's default)"),
+                "region lists in their table (round 5's default)") if others else None,
+            "no_speculation": self._form_summary(
+                ms_ns, ns_acl, ns_reg, "the default forms with the context param speculate 0: ACL "
+                "entry flags checked in the walk, no guarded second launch") if others else None,
             "calls": "honu_decode_batch(data arena NULL) over all records, one call",
             "roofline": {
                 "bound": "hbm",

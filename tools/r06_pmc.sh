@@ -26,7 +26,7 @@ run() {  # name workload args...
 if [ "$part" = 1 ]; then
   run pmc_large "1048576 large records per GPU: $ED" $NL || exit 1
   run pmc_zc "1048576 large records per GPU: decode (Object.Metadata + Object.Data) of one resident records arena, zero_copy" \
-    --mode decode --decode-leg zero_copy --no-cpu-baseline --no-host-path --legs none || exit 2
+    --mode decode --decode-leg zero_copy --zc-forms default --no-cpu-baseline --no-host-path --legs none || exit 2
   run pmc_mat "1048576 large records per GPU: decode (Object.Metadata + Object.Data) of one resident records arena, materialising" \
     --mode decode --decode-leg materialising --no-cpu-baseline --no-host-path --legs none || exit 3
   run pmc_small "1048576 small records per GPU: $ED" --shape small $NL || exit 4
