@@ -114,6 +114,10 @@ def parse_args(argv=None):
                         "medium (1M Medium encode + decode), xlarge (--records/16 XLarge encode + "
                         "decode + chunk zero copy); auto: all four for the default Large line, none "
                         "otherwise; none: no legs")
+    p.add_argument("--guard-blocks", type=int, default=-1,
+                   help="context param guard_blocks of the output slots: one-wave workgroups of the "
+                        "single-launch decode's guarded launch (0: as many as the speculative launch "
+                        "has waves; -1: the library default)")
     p.add_argument("--decode-prio", type=int, default=0, choices=[0, 1],
                    help="1: a chunk's single-launch decode (and its guarded launch) on a high-priority "
                         "stream of its slot, so the guard's workgroups are dispatched before the other "
@@ -259,6 +263,9 @@ class Bench:
             if args.copy_blocks:
                 _lib.check(self.lib.honu_ctx_set_param(sl.codec.ctx, b"copy_blocks",
                                                        args.copy_blocks * ncu), "param")
+            if getattr(args, "guard_blocks", -1) >= 0:
+                _lib.check(self.lib.honu_ctx_set_param(sl.codec.ctx, b"guard_blocks",
+                                                       args.guard_blocks), "param")
         if not args.serial:
             for sl in self.slots:
                 if args.meta_blocks:
