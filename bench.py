@@ -1081,7 +1081,7 @@ def pmc_commit(workload):
     return _pmc_entry(workload).get("commit")
 
 
-def hbm_probe(codec, dev, nbytes=4 << 30, reps=5):
+def hbm_probe(codec, dev, nbytes=4 << 30, reps=5, modes=(0, 1, 2, 3, 4), blocks=(1, 2, 4)):
     """The part's achievable streaming rates, measured in this process with the
     library's own probe kernels (honu_hbm_probe: 16 B per lane, the layout of
     tools/hbm_probe.hip and of the guide's float4 copy): read-only, write-only
@@ -1111,10 +1111,12 @@ def hbm_probe(codec, dev, nbytes=4 << 30, reps=5):
         return (2 if mode >= 2 else 1) * nbytes / t / 1e9
 
     out = {"bytes": nbytes, "reps": reps}
-    out["read_gbs"] = max(rate(0, k) for k in (1, 2, 4))
-    out["write_gbs"] = max(rate(1, k) for k in (1, 2, 4))
+    if 0 in modes:
+        out["read_gbs"] = max(rate(0, k) for k in blocks)
+    if 1 in modes:
+        out["write_gbs"] = max(rate(1, k) for k in blocks)
     forms = {2: "wave ranges", 3: "grid stride", 4: "wave ranges, non-temporal"}
-    best = max(((rate(m, k), m, k) for m in (2, 3, 4) for k in (1, 2, 4)), key=lambda x: x[0])
+    best = max(((rate(m, k), m, k) for m in (2, 3, 4) if m in modes for k in blocks), key=lambda x: x[0])
     out["copy_gbs"], out["copy_form"] = best[0], f"{forms[best[1]]}, {best[2]} workgroups per CU"
     del a, b
     torch.cuda.empty_cache()
@@ -1708,6 +1710,11 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
     bench.payload = None  # the scatter leg keeps the output slots, nothing else
     gc.collect()
     torch.cuda.empty_cache()
+    # the probe's copy forms over as many bytes as one payload copy launch
+    # moves (the 4 GiB probe's best form is faster than any
+    # copy of a chunk's 2 x 12 GB; profiles/r06/copy_attr/)
+    probe_chunk = hbm_probe(bench.codec, bench.dev, nbytes=max(bench.chunk_payload) // 16 * 16, reps=3,
+                            modes=(2, 4), blocks=(1, 2))
     scatter = None
     if dist is not None:
         arena = off = None
@@ -1727,6 +1734,8 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
         mr = decode["materialising"]["roofline"]
         mr["achievable"] = probe["copy_gbs"]
         mr["frac_of_achievable"] = mr["achieved"] / probe["copy_gbs"]
+        mr["achievable_at_launch_bytes"] = probe_chunk["copy_gbs"]
+        mr["frac_of_achievable_at_launch_bytes"] = mr["achieved"] / probe_chunk["copy_gbs"]
     step_s = elapsed / args.steps
     total_bytes, total_records = tot
     launches = len(dec_ms)
@@ -1787,6 +1796,8 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
             "frac": dom_gbs / HBM_PEAK_GBS,
             "achievable": probe["copy_gbs"],
             "frac_of_achievable": dom_gbs / probe["copy_gbs"],
+            "achievable_at_launch_bytes": probe_chunk["copy_gbs"],
+            "frac_of_achievable_at_launch_bytes": dom_gbs / probe_chunk["copy_gbs"],
             "traffic": traffic,
             "traffic_source": "profiles/pmc_traffic.json" if traffic else None,
             "traffic_commit": pmc_commit(workload),
@@ -1801,6 +1812,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
             "decode_copy_ms_per_step": sum(dec_ms) / args.steps,
             "step_hbm_gbs_algorithmic": 4 * bench.total_rec_bytes / step_s / 1e9,
             "hbm_probe": probe,
+            "hbm_probe_at_launch_bytes": probe_chunk,
             "zero_copy_decode_records_per_s": zc["records_per_s"],
             "zero_copy_decode_ms_per_chunk": zc["ms"],
             "zero_copy_decode_chunk_records": zc["records"],

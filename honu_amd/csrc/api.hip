@@ -22,7 +22,7 @@ struct honu_ctx {
     uint64_t *totals;        // 4 (3: decode totals; word 3: the HBM probe's sink)
     DecodeScratch *scratch;  // max_n
     uint32_t *reg_inline;    // 8 * max_n: region ids handed from the group parse to fill
-    uint64_t *enc_acl;       // max_n: ACL list positions, lane encoder -> group ACL encoder
+    EncAclPos *enc_acl;      // max_n: ACL list hand-over, lane encoder -> group ACL encoder
     // decoupled look-back state of the fused decode (fused.hip): a
     // ticket/epoch block and 3 status words per 64-record tile
     LbState *lb_dec;
@@ -237,7 +237,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     const uint64_t lb_bytes =
         2 * sizeof(LbState) + 8 * (lb_dec_words + scan_words) + COPY_TICKET_LINES * 4 * COPY_TICKET_STRIDE;
     const uint64_t bytes = 8 * (3 * n + 3 * n + 4 + np) + sizeof(DecodeScratch) * n + 32 * n +
-                           8 * n + 4 * map_cap + lb_bytes + 256;
+                           sizeof(EncAclPos) * n + 4 * map_cap + lb_bytes + 256;
     if (hipMalloc(&c->ws, bytes) != hipSuccess) {
         c->ws = nullptr;
         char msg[96];
@@ -275,7 +275,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     w += 4;
     c->scratch = (DecodeScratch *)w;
     c->reg_inline = (uint32_t *)(c->scratch + n);
-    c->enc_acl = (uint64_t *)(c->reg_inline + 8 * n);
+    c->enc_acl = (EncAclPos *)(c->reg_inline + 8 * n);
     c->geom.tile_map = (uint32_t *)(c->enc_acl + n);
     c->geom.tile_map_cap = map_cap;
     c->lb_dec = (LbState *)(c->geom.tile_map + map_cap);

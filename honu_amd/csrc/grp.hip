@@ -238,20 +238,34 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_decode_fill_grp(
 template <int G, bool SELF>
 HONU_DEV void k_encode_acl_grp_one(uint64_t i, const honu_meta *__restrict__ meta, const honu_acl *__restrict__ acl, uint64_t n,
     uint8_t *__restrict__ out, int32_t *__restrict__ status,
-    const uint64_t *__restrict__ acl_pos, const uint64_t *__restrict__ payload_off,
+    const EncAclPos *__restrict__ acl_pos, const uint64_t *__restrict__ payload_off,
     const uint64_t *__restrict__ out_off, uint64_t out_cap) {
     const uint32_t r = threadIdx.x & (G - 1);
-    // independent loads first: one round trip before the entries
+    // independent loads first: one round trip before the entries. After the
+    // lane encoder (!SELF) its 32-byte hand-over holds the row fields needed
+    // here, so the row itself is not read again.
     const int32_t sti = status[i];
-    const honu_meta &m = meta[i];
-    const uint64_t na = m.acl_count, ao = m.acl_off;
+    uint64_t na, ao, carried;
+    bool sized;
+    if constexpr (SELF) {
+        const honu_meta &m = meta[i];
+        na = m.acl_count;
+        ao = m.acl_off;
+        sized = (m.present & HONU_ACL_SIZED) != 0;
+        carried = m.acl_bytes;
+    } else {
+        const EncAclPos h = acl_pos[i];
+        na = h.acl_count;
+        ao = h.acl_off;
+        sized = (h.carried & ENC_ACL_SIZED) != 0;
+        carried = h.carried & ~ENC_ACL_SIZED;
+    }
     // a carried list length (HONU_ACL_SIZED) sized the record: every entry is
     // read below anyway, so the length is checked here (a row that lies gets
     // HONU_ERR_INPUT; its range of the output is then unspecified)
-    const bool sized = (m.present & HONU_ACL_SIZED) != 0;
-    const uint64_t carried = m.acl_bytes;
     uint64_t pos;
     if constexpr (SELF) {
+        const honu_meta &m = meta[i];
         const uint64_t beg = out_off[i], end = out_off[i + 1];
         if (sti != HONU_OK || !na || end > out_cap) return;  // (the lane encoder flags the capacity)
         const uint32_t pr = m.present;
@@ -275,8 +289,8 @@ HONU_DEV void k_encode_acl_grp_one(uint64_t i, const honu_meta *__restrict__ met
         }
         pos = (beg + 1 + uvarint_len(dlen) + dlen + t) | (miss == 0 ? ACL_ALL_PRESENT : 0);
     } else {
-        pos = acl_pos[i];
         if (sti != HONU_OK || !na) return;
+        pos = acl_pos[i].pos;
     }
     const honu_acl *A = acl + ao;
     const uint64_t P = pos & ~ACL_ALL_PRESENT;
@@ -331,7 +345,7 @@ template <int G, bool SELF>
 __global__ __launch_bounds__(HONU_BLOCK) void k_encode_acl_grp(
     const honu_meta *__restrict__ meta, const honu_acl *__restrict__ acl, uint64_t n,
     uint8_t *__restrict__ out, int32_t *__restrict__ status,
-    const uint64_t *__restrict__ acl_pos, const uint64_t *__restrict__ payload_off,
+    const EncAclPos *__restrict__ acl_pos, const uint64_t *__restrict__ payload_off,
     const uint64_t *__restrict__ out_off, uint64_t out_cap) {
     for (uint64_t i = ((uint64_t)blockIdx.x * HONU_BLOCK + threadIdx.x) / G; i < n;
          i += (uint64_t)gridDim.x * (HONU_BLOCK / G))
@@ -351,7 +365,7 @@ hipError_t launch_encode_sizes_grp(const honu_meta *meta, uint64_t var_len, cons
 }
 
 hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uint64_t n,
-                                 uint8_t *out, int32_t *status, const uint64_t *acl_pos,
+                                 uint8_t *out, int32_t *status, const EncAclPos *acl_pos,
                                  int max_blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL((k_encode_acl_grp<GRP, false>), grp_grid(n, max_blocks), dim3(HONU_BLOCK), 0, s, meta, acl,

@@ -119,15 +119,26 @@ hipError_t launch_decode_keys(const LaunchGeom &g, const honu_meta *meta,
                               const honu_record_info *info, uint64_t n, uint8_t *keys,
                               int32_t *key_status, hipStream_t s);
 
-// acl_out != null: the ACL entries are left out (positions in acl_out) for
+// The lane encoder's hand-over to the ACL list kernel, one per record: where
+// the list goes (| ACL_ALL_PRESENT) and the row fields the list kernel needs,
+// so that it reads 32 bytes per record instead of two lines of the row.
+struct EncAclPos {
+    uint64_t pos;        // the list's first byte in the output (| ACL_ALL_PRESENT)
+    uint64_t acl_off;    // the row's acl_off / acl_count
+    uint64_t acl_count;
+    uint64_t carried;    // the row's acl_bytes | ENC_ACL_SIZED when HONU_ACL_SIZED is set
+};
+#define ENC_ACL_SIZED (1ull << 63)
+
+// acl_out != null: the ACL entries are left out (hand-over in acl_out) for
 // launch_encode_acl_grp
 hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
                                    const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
                                    uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
-                                   int32_t *status, uint64_t *acl_out, int max_blocks, int num_cu,
+                                   int32_t *status, EncAclPos *acl_out, int max_blocks, int num_cu,
                                    const uint8_t *payload, hipStream_t s);
 hipError_t launch_encode_acl_grp(const honu_meta *meta, const honu_acl *acl, uint64_t n,
-                                 uint8_t *out, int32_t *status, const uint64_t *acl_pos,
+                                 uint8_t *out, int32_t *status, const EncAclPos *acl_pos,
                                  int max_blocks, hipStream_t s);
 // the same with the lists placed by the kernel itself (no acl_pos), so that it
 // can run beside launch_encode_meta_lane

@@ -33,7 +33,7 @@ HONU_DEV void k_encode_meta_lane_one(uint64_t i, const honu_meta &m, const uint8
     const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
     const uint64_t *__restrict__ payload_off, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status,
-    uint64_t *__restrict__ acl_out, u32x4 *ring, const uint8_t *__restrict__ payload) {
+    EncAclPos *__restrict__ acl_out, u32x4 *ring, const uint8_t *__restrict__ payload) {
     if (status[i] != HONU_OK) return;
     const uint64_t beg = out_off[i], end = out_off[i + 1];
     if (end > out_cap) {
@@ -43,7 +43,9 @@ HONU_DEV void k_encode_meta_lane_one(uint64_t i, const honu_meta &m, const uint8
     const uint64_t dlen = payload_off[i + 1] - payload_off[i];
     const uint64_t pos = encode_record_lane<SKIP_ACL, SKIP_ACL ? RING : 0>(
         m, var, acl, reg, dlen, beg, end, out, ring, payload ? payload + payload_off[i] : nullptr);
-    if constexpr (SKIP_ACL) acl_out[i] = pos;
+    if constexpr (SKIP_ACL)
+        acl_out[i] = EncAclPos{pos, m.acl_off, m.acl_count,
+                               m.acl_bytes | ((m.present & HONU_ACL_SIZED) ? ENC_ACL_SIZED : 0)};
 }
 
 // a lane's row straight from global memory (the loads cannot pass the output
@@ -61,7 +63,7 @@ __global__ __launch_bounds__(HONU_BLOCK) void k_encode_meta_lane(
     const honu_acl *__restrict__ acl, const uint32_t *__restrict__ reg,
     const uint64_t *__restrict__ payload_off, uint64_t n, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint64_t *__restrict__ out_off, int32_t *__restrict__ status,
-    uint64_t *__restrict__ acl_out, const uint8_t *__restrict__ payload) {
+    EncAclPos *__restrict__ acl_out, const uint8_t *__restrict__ payload) {
     constexpr uint32_t WAVE_BYTES = enc_wave_bytes<RING>();
     __shared__ __attribute__((aligned(16))) uint8_t smem[HONU_WAVES_PER_BLOCK * WAVE_BYTES];
     uint8_t *area = smem + (threadIdx.x / HONU_WAVE) * WAVE_BYTES;
@@ -197,7 +199,7 @@ static dim3 lane_grid(uint64_t n, int cap) {
 hipError_t launch_encode_meta_lane(const honu_meta *meta, const uint8_t *var, const honu_acl *acl,
                                    const uint32_t *reg, const uint64_t *payload_off, uint64_t n,
                                    uint8_t *out, uint64_t out_cap, const uint64_t *out_off,
-                                   int32_t *status, uint64_t *acl_out, int max_blocks, int num_cu,
+                                   int32_t *status, EncAclPos *acl_out, int max_blocks, int num_cu,
                                    const uint8_t *payload, hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (!acl_out) return hipErrorInvalidValue;
