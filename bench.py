@@ -792,15 +792,18 @@ class DecodeBench:
         torch.cuda.synchronize()
         return [x.elapsed_time(y) for x, y in ev]
 
-    def _form_reps(self, acl, reg, reps, speculate=1):
+    def _form_reps(self, acl, reg, reps, speculate=None):
         """reps timed calls with the context params acl_inplace / regions_inplace
         set to (acl, reg): (per-call ms, ACL table entries, region table entries)."""
         c = self.codec.ctx
         _lib.check(self.lib.honu_ctx_set_param(c, b"acl_inplace", acl), "param")
         _lib.check(self.lib.honu_ctx_set_param(c, b"regions_inplace", reg), "param")
-        _lib.check(self.lib.honu_ctx_set_param(c, b"speculate", speculate), "param")
+        old = ctypes.c_int64(1)
+        _lib.check(self.lib.honu_ctx_get_param(c, b"speculate", ctypes.byref(old)), "param")
+        if speculate is not None:
+            _lib.check(self.lib.honu_ctx_set_param(c, b"speculate", speculate), "param")
         ms = self._zero_copy_reps(reps)
-        _lib.check(self.lib.honu_ctx_set_param(c, b"speculate", 1), "param")
+        _lib.check(self.lib.honu_ctx_set_param(c, b"speculate", old.value), "param")
         tt = self.totals[:16].view(torch.int64).tolist()
         return ms, int(tt[0]), int(tt[1])
 

@@ -37,7 +37,7 @@ struct honu_ctx {
     // of batches with malformed records pays ~1.1x instead of ~2x per batch
     uint32_t *spec_seen;     // pinned: [0] the back-off flag, [1] recovery launches run (a count)
     uint32_t spec_off;       // calls left without speculation
-    bool spec_allowed;       // honu_ctx_set_param("speculate", 0) turns it off
+    int speculate;           // honu_ctx_set_param("speculate"): 0 off, 1 on, 2 where it hides a wait
     // honu_encode_records: the ACL lists' kernel on a stream of the context's
     // own, beside the header/tail encoder (forked from and joined back into
     // the caller's stream by events)
@@ -64,6 +64,9 @@ static LaunchGeom copy_geom(honu_ctx *ctx) {
     return g;
 }
 static constexpr uint32_t SPEC_BACKOFF_CALLS = 16;
+#ifndef SPECULATE_DEFAULT
+#define SPECULATE_DEFAULT 1
+#endif
 
 static thread_local char g_last_error[256];
 
@@ -251,7 +254,7 @@ honu_ctx *honu_ctx_create(int device, uint64_t max_records, int32_t *err) {
     }
     c->spec_seen[0] = 0;
     c->spec_seen[1] = 0;
-    c->spec_allowed = true;
+    c->speculate = SPECULATE_DEFAULT;
     c->enc_fork = env_int("HONU_ENCODE_FORK", 2);
     if (c->enc_fork < 0 || c->enc_fork > 2) c->enc_fork = 2;
     if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) {
@@ -327,7 +330,7 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value) {
     if (!strcmp(name, "copy_blocks") && value > 0) ctx->geom.copy_blocks = (int)value;
     else if (!strcmp(name, "record_blocks") && value > 0) ctx->geom.per_record_blocks = (int)value;
     else if (!strcmp(name, "lane_blocks") && value >= 0) ctx->geom.lane_blocks = (int)value;
-    else if (!strcmp(name, "speculate") && (value == 0 || value == 1)) ctx->spec_allowed = value != 0;
+    else if (!strcmp(name, "speculate") && value >= 0 && value <= 2) ctx->speculate = (int)value;
     else if (!strcmp(name, "encode_fork") && value >= 0 && value <= 2) ctx->enc_fork = (int)value;
     else if (!strcmp(name, "acl_inplace") && (value == 0 || value == 1)) ctx->acl_inplace = value != 0;
     else if (!strcmp(name, "regions_inplace") && (value == 0 || value == 1)) ctx->reg_inplace = value != 0;
@@ -354,7 +357,7 @@ int32_t honu_ctx_get_param(const honu_ctx *ctx, const char *name, int64_t *value
     if (!strcmp(name, "copy_blocks")) *value = ctx->geom.copy_blocks;
     else if (!strcmp(name, "record_blocks")) *value = ctx->geom.per_record_blocks;
     else if (!strcmp(name, "lane_blocks")) *value = ctx->geom.lane_blocks;
-    else if (!strcmp(name, "speculate")) *value = ctx->spec_allowed ? 1 : 0;
+    else if (!strcmp(name, "speculate")) *value = ctx->speculate;
     else if (!strcmp(name, "encode_fork")) *value = ctx->enc_fork;
     else if (!strcmp(name, "acl_inplace")) *value = ctx->acl_inplace ? 1 : 0;
     else if (!strcmp(name, "regions_inplace")) *value = ctx->reg_inplace ? 1 : 0;
@@ -626,7 +629,13 @@ int32_t honu_decode_records(honu_ctx *ctx, const uint8_t *d_rec, const uint64_t 
         __atomic_store_n(ctx->spec_seen, 0u, __ATOMIC_RELAXED);
         ctx->spec_off = SPEC_BACKOFF_CALLS;
     }
-    const bool spec = ctx->spec_allowed && ctx->spec_off == 0;
+    // speculation hides the look-back wait; a zero-copy call with both list
+    // forms in place has none to hide (fused.hip: tiles without table entries
+    // do not wait), so "speculate" 2 (auto) decodes it without speculation:
+    // no ACL flag burst after the walk re-reading the list's lines, no guarded
+    // second launch
+    const bool hides = materialize || !ctx->acl_inplace || !ctx->reg_inplace;
+    const bool spec = (ctx->speculate == 1 || (ctx->speculate == 2 && hides)) && ctx->spec_off == 0;
     if (ctx->spec_off) ctx->spec_off--;
     HIPCHK(launch_decode_fused(d_rec, d_rec_off, n, d_meta, d_info, d_acl, acl_cap, d_regions,
                                regions_cap, materialize != 0, data_cap, ctx->scratch, ctx->offs,
