@@ -145,6 +145,9 @@ def parse_args(argv=None):
                    help="decode legs: the zero-copy leg times the default list forms and, for "
                         "comparison, the table forms and speculation off (all), or the default forms "
                         "only (default: PMC passes, whose per-kernel averages would mix the forms)")
+    p.add_argument("--zc-speculate", type=int, default=-1, choices=[-1, 0, 1, 2],
+                   help="the zero-copy leg's context param speculate for the default forms (-1: the "
+                        "library default)")
     p.add_argument("--no-host-path", action="store_true",
                    help="encdec mode: skip the host-path leg (PMC passes: its small launches "
                         "would mix into the copy kernels' per-launch averages)")
@@ -824,12 +827,14 @@ class DecodeBench:
         default's reps split around the others."""
         h = max(1, reps // 2)
         others = getattr(self.args, "zc_forms", "all") == "all"
-        ms = self._form_reps(1, 1, h)[0]
+        sp = getattr(self.args, "zc_speculate", -1)
+        sp = None if sp < 0 else sp
+        ms = self._form_reps(1, 1, h, speculate=sp)[0]
         if others:
             ms_tab, tab_acl, tab_reg = self._form_reps(0, 0, reps)
             ms_r5, r5_acl, r5_reg = self._form_reps(1, 0, reps)
             ms_ns, ns_acl, ns_reg = self._form_reps(1, 1, reps, speculate=0)
-        ms2, acl_e, reg_e = self._form_reps(1, 1, reps - h)
+        ms2, acl_e, reg_e = self._form_reps(1, 1, reps - h, speculate=sp)
         ms = ms + ms2
         t = sum(ms) / len(ms) / 1e3
         N = self.b.N
