@@ -419,3 +419,46 @@ def test_speculated_long_list_checked_under_capacity_failure(oracle_lib, inplace
         assert d.reg[:4 * nreg].cpu().numpy().tobytes() == oreg[:nreg].tobytes()
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("inplace", [1, 0], ids=["lists_inplace", "lists_table"])
+def test_speculate_auto(oracle_lib, inplace):
+    """Context param speculate 2 (auto): speculation only where it hides a
+    look-back wait. A zero-copy call with both list forms in place waits for
+    nothing, so it decodes without speculation: a 2188-tile batch with nil ACL
+    entries spliced in decodes bit-exact with no recovery launch; with the
+    table forms the same call speculates and recovers once. The param reads
+    back, and values outside 0..2 are refused."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from corpora import random_metas
+    from honu_amd.metadata import pack_batch
+    n = 140000
+    rec, off, _ = oracle_lib.marshal_batch(gen_host_batch(47, "small", 0, n))
+    metas, datas = random_metas(200, 79)
+    pick = [i for i, m in enumerate(metas) if m.ACL and any(a is None for a in m.ACL) and datas[i]][:20]
+    r2, o2, _ = oracle_lib.marshal_batch(pack_batch([metas[i] for i in pick], [datas[i] for i in pick]))
+    at = set(int(x) for x in np.linspace(5, n - 1, len(pick)).astype(np.int64))
+    pieces, noff, j = [], [0], 0
+    for i in range(n):
+        if i in at:
+            r = r2[int(o2[j]):int(o2[j + 1])]
+            j += 1
+        else:
+            r = rec[int(off[i]):int(off[i + 1])]
+        pieces.append(r)
+        noff.append(noff[-1] + len(r))
+    brec, boff = np.concatenate(pieces), np.array(noff, np.uint64)
+    c = hobj.Codec(0, n)
+    try:
+        hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
+        assert c.lib.honu_ctx_set_param(c.ctx, b"speculate", 3) != 0
+        hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"speculate", 2), "param")
+        assert _get(c, b"speculate") == 2
+        r0 = _get(c, b"recoveries")
+        d = _Dec(c, brec, boff, inplace)
+        assert d() == 0
+        d.check(oracle_lib, brec, boff)
+        assert _get(c, b"recoveries") == r0 + (0 if inplace == 1 else 1)
+    finally:
+        c.close()
