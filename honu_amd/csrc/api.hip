@@ -64,8 +64,12 @@ static LaunchGeom copy_geom(honu_ctx *ctx) {
     return g;
 }
 static constexpr uint32_t SPEC_BACKOFF_CALLS = 16;
+// Speculation only where it hides a look-back wait (materialising decodes,
+// table forms): a zero-copy in-place launch skips those waits already, and
+// there the flag gather and guard cost more than the walk's own flag check
+// (round 6: 0.392 vs 0.427 ms for 1M Large records, profiles/r06).
 #ifndef SPECULATE_DEFAULT
-#define SPECULATE_DEFAULT 1
+#define SPECULATE_DEFAULT 2
 #endif
 
 static thread_local char g_last_error[256];

@@ -265,9 +265,10 @@ int32_t honu_ctx_reset(honu_ctx *ctx, void *stream);
  * size; 6 the single-launch decode at every size), "encode_variant" (the
  * header/tail encoder of honu_encode_records: 0 one record per lane + the ACL
  * lists by 16-lane groups, the default; 1 one record per 16-lane group laid
- * out by a prefix sum over the grammar's slots, same bytes), "speculate" (1
- * default, 0 off: the single-launch decode's speculation, see
- * honu_decode_records), "speculate_backoff" (0..16: the calls left without
+ * out by a prefix sum over the grammar's slots, same bytes), "speculate" (the
+ * single-launch decode's speculation, see honu_decode_records: 2 auto, the
+ * default — only in materialising calls and the table forms, where it hides
+ * look-back waits; 1 in every call; 0 off), "speculate_backoff" (0..16: the calls left without
  * speculation after a recovery; setting it also forgets a recovery the host
  * has not seen yet), "encode_fork" (honu_encode_records: 1 runs the ACL lists'
  * kernel, which then places the lists itself, on a stream of the context's own
@@ -433,7 +434,9 @@ int32_t honu_decode_payloads(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n,
  * subslice of the records arena (Object.Data, object.go:85-99). Results are
  * identical to the split path's. Launches of 768 or more 64-record tiles
  * speculate (counts published before the walk ends, ACL entry flags checked
- * by the table fill); a batch holding any record that fails after its counts
+ * by the table fill or a gather after the publish) when the param
+ * "speculate" allows it — by default materialising calls and the table forms,
+ * not a zero-copy call with both lists in place; a batch holding any record that fails after its counts
  * were published, or a nil ACL entry, is decoded a second time without
  * speculation inside the same call, so such a batch costs about twice a
  * clean one (malformed input and nil entries only; results are exact either

@@ -48,6 +48,13 @@ def _oracle(oracle_lib, rec, off, inplace, materialize=False):
     return oracle_lib.decode_batch(rec, off, materialize, bool(acl), bool(reg))
 
 
+def _speculative(c):
+    """The single-launch decode with speculation on in every form (speculate
+    1; the default 2 leaves the zero-copy in-place forms without it)."""
+    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
+    hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"speculate", 1), "param")
+
+
 def _dev(a, codec):
     return hobj._dev_bytes(np.ascontiguousarray(a), codec.torch_device)
 
@@ -203,7 +210,7 @@ def test_speculative_publish_recovers(oracle_lib, n, bad, inplace):
     boff = np.array(noff, np.uint64)
     c = hobj.Codec(0, n)
     try:
-        hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
+        _speculative(c)
         d = _Dec(c, brec, boff, inplace)
         assert d() == 0
         d.check(oracle_lib, brec, boff)
@@ -258,7 +265,7 @@ def test_speculative_acl_flags_recover(oracle_lib, n, k, inplace, inline_rec, gu
     brec, boff = np.concatenate(pieces), np.array(noff, np.uint64)
     c = hobj.Codec(0, n)
     try:
-        hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
+        _speculative(c)
         hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"inline_recovery", inline_rec), "param")
         hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"guard_blocks", guard_blocks), "param")
         r0 = _get(c, b"recoveries")
@@ -305,7 +312,7 @@ def test_speculation_backs_off_after_a_recovery(oracle_lib):
         hobj._lib.check(c.lib.honu_ctx_get_param(c.ctx, name, C.byref(v)), "get_param")
         return v.value
     try:
-        hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
+        _speculative(c)
         d, good = _Dec(c, brec, boff), _Dec(c, rec, off)
         assert get(b"speculate") == 1 and get(b"speculate_backoff") == 0
         assert good() == 0
@@ -349,6 +356,8 @@ def test_concurrent_ticket_and_static_launches_on_two_streams(oracle_lib):
     b3 = oracle_lib.marshal_batch(gen_host_batch(53, "small", 0, n_static))
     c1, c2 = hobj.Codec(0, n_ticket), hobj.Codec(0, n_ticket)
     try:
+        for c in (c1, c2):  # speculative ticket launches beside each other
+            hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"speculate", 1), "param")
         d1, d2, d3 = _Dec(c1, *b1[:2]), _Dec(c2, *b2[:2]), _Dec(c2, *b3[:2])
         s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
         torch.cuda.synchronize()
@@ -398,7 +407,7 @@ def test_speculated_long_list_checked_under_capacity_failure(oracle_lib, inplace
     acl_cap, reg_cap = int(otot[0]) - 1, int(otot[1]) + 16
     c = hobj.Codec(0, n)
     try:
-        hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
+        _speculative(c)
         d = _Dec(c, brec, boff, inplace)
         d.acl_cap, d.reg_cap = acl_cap, reg_cap
         assert d() == 0
@@ -452,6 +461,7 @@ def test_speculate_auto(oracle_lib, inplace):
     c = hobj.Codec(0, n)
     try:
         hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
+        assert _get(c, b"speculate") == 2  # the default
         assert c.lib.honu_ctx_set_param(c.ctx, b"speculate", 3) != 0
         hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"speculate", 2), "param")
         assert _get(c, b"speculate") == 2
