@@ -114,6 +114,9 @@ def parse_args(argv=None):
                         "medium (1M Medium encode + decode), xlarge (--records/16 XLarge encode + "
                         "decode + chunk zero copy); auto: all four for the default Large line, none "
                         "otherwise; none: no legs")
+    p.add_argument("--leg-pause", type=float, default=0.0,
+                   help="seconds the device idles before each leg (a probe of whether a leg's time "
+                        "depends on the load before it; 0: none)")
     p.add_argument("--guard-blocks", type=int, default=-1,
                    help="context param guard_blocks of the output slots: one-wave workgroups of the "
                         "single-launch decode's guarded launch (0: as many as the speculative launch "
@@ -1623,6 +1626,9 @@ def run_legs(args, rank, local, world, dist, barrier, gather_max, all_ok):
         shape, enc, frac, zc = LEG_SHAPES[name]
         gc.collect()
         torch.cuda.empty_cache()
+        if args.leg_pause > 0:
+            torch.cuda.synchronize()
+            time.sleep(args.leg_pause)
         legs[name] = pipeline_leg(args, shape, enc, rank, local, world, dist, barrier, gather_max,
                                   all_ok, records=max(1, int(args.records * frac)), zero_copy=zc)
     return legs or None

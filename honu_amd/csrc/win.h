@@ -40,6 +40,15 @@ constexpr uint32_t WSL = WB / 16 + 1;  // LDS stride in 16-byte slots: one pad s
                                        // on different banks
 constexpr uint32_t WS = WSL * 16;
 constexpr uint64_t NOWIN = ~0ull;
+// Where a window starts: the 16-byte block holding the walk's position, or
+// (HONU_WIN_ALIGN 64 / 128, an A/B build) the memory unit holding it, so
+// that a window never ends inside a unit the next refill fetches again.
+#ifndef HONU_WIN_ALIGN
+#define HONU_WIN_ALIGN 16
+#endif
+static_assert(HONU_WIN_ALIGN >= 16 && HONU_WIN_ALIGN <= 128 && (HONU_WIN_ALIGN & (HONU_WIN_ALIGN - 1)) == 0,
+              "a power of two from a block to half the window");
+HONU_DEV uint64_t win_base(uint64_t p) { return p & ~(uint64_t)(HONU_WIN_ALIGN - 1); }
 // windows + per-lane wanted base, previous base and fetch limit
 constexpr uint32_t WIN_WAVE_BYTES = HONU_WAVE * WS + 3 * HONU_WAVE * 8;
 // The ACL flag gathers (the walk below, fused.hip flag_gather): lane k's flags
@@ -413,7 +422,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
     D.tstart = st == HONU_OK ? beg + 1 + (uint64_t)b + (uint64_t)d : 0;
     D.p = D.tstart;
     WSTAMP(2);  // header read
-    W.refill(st == HONU_OK ? (D.p & ~15ull) : NOWIN);
+    W.refill(st == HONU_OK ? win_base(D.p) : NOWIN);
     WSTAMP(3);  // first window
 
     uint32_t f = 0, u = 0, pr = 0;
@@ -510,7 +519,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
     if (!spec_acl) {
         bool chk = fast && ak < nacl;
         while (__ballot(chk)) {
-            W.refill(chk ? ((D.p + 18 * ak) & ~15ull) : NOWIN);
+            W.refill(chk ? win_base(D.p + 18 * ak) : NOWIN);
             if (chk) {
                 // the flags this window holds (at most 15), read independently
                 const uint64_t q = D.p + 18 * ak;
@@ -548,7 +557,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
     }
     if (hm) R.u64(OFF(acl_count), nacl);  // 0 for an empty list (metadata.go:254)
     WSTAMP(5);  // ACL flags checked
-    W.refill(hm && st == HONU_OK ? (D.p & ~15ull) : NOWIN);
+    W.refill(hm && st == HONU_OK ? win_base(D.p) : NOWIN);
     WSTAMP(6);  // window after the list
     if (hm) {
         STEP(D.u64(nreg));                                  // region.go:154-169
@@ -604,7 +613,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
         }
     }
     WSTAMP(7);  // regions .. signature
-    W.refill(hm && st == HONU_OK ? (D.p & ~15ull) : NOWIN);
+    W.refill(hm && st == HONU_OK ? win_base(D.p) : NOWIN);
     WSTAMP(8);  // window after the signature
     if (hm) {
         if (has_enc) {
