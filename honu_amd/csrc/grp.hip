@@ -308,6 +308,21 @@ HONU_DEV void k_encode_acl_grp_one(uint64_t i, const honu_meta *__restrict__ met
         const uint64_t ab = (uint64_t)out;
         const uint64_t X0 = ((ab + P + ACL_UNIT - 1) & ~(ACL_UNIT - 1)) - ab,
                        X1 = ((ab + P + 18 * na) & ~(ACL_UNIT - 1)) - ab;
+        if constexpr (HONU_ACL_ENDS && ACL_UNIT == 16) {
+            // the partial chunks at both ends ([P, X0) and [X1, E): fewer than
+            // 16 bytes each; a list is >= 18 bytes, so X0 <= X1), byte stores by
+            // two lanes of the group
+            const uint64_t E = P + 18 * na;
+            const uint64_t x = r == 0 ? P : X1;
+            const uint32_t cnt = (uint32_t)(r == 0 ? X0 - P : E - X1);
+            if (r < 2 && cnt) {
+                const u32x4 v = acl_chunk(A, na, P, x);
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (uint32_t b = 0; b < 15; b++)
+                    if (b < cnt) out[x + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+            }
+        }
         if (X1 <= X0) return;
         const uint64_t nch = (X1 - X0) >> 4;
         constexpr int K = 2;  // chunks per lane computed before any store

@@ -420,6 +420,12 @@ HONU_DEV uint64_t ld64(const uint8_t *p) { return *reinterpret_cast<const uint64
 #ifndef ACL_UNIT
 #define ACL_UNIT 16ull
 #endif
+// HONU_ACL_ENDS 1: the list kernel also writes the list's bytes in the partial
+// 16-byte chunks at its two ends (byte stores), so this lane reads no ACL
+// entry at all; 0: this lane writes them (ACL_UNIT 16).
+#ifndef HONU_ACL_ENDS
+#define HONU_ACL_ENDS 0
+#endif
 // Header + Metadata tail of one record into out[beg, end) (the payload bytes
 // in between are the copy engine's). SKIP_ACL: leave the ACL entries to a
 // group writer: write the fields up to uvarint(len ACL), return that position
@@ -555,7 +561,9 @@ HONU_DEV uint64_t encode_record_lane(const honu_meta &m, const uint8_t *__restri
             };
             // (acl_chunk: 16 bytes of the list's encoding from x, from the
             // <= 2 entries they straddle)
-            if constexpr (ACL_UNIT == 16) {  // one piece of < 16 bytes at each end, both loaded at once
+            if constexpr (HONU_ACL_ENDS && ACL_UNIT == 16) {  // the list kernel's, ends included
+                W.jump(E);
+            } else if constexpr (ACL_UNIT == 16) {  // one piece of < 16 bytes at each end, both loaded at once
                 const u32x4 hv = acl_chunk(acl + ao, na, P, P);
                 const u32x4 tv = E > T ? acl_chunk(acl + ao, na, P, T) : u32x4{0, 0, 0, 0};
                 put_n(hv, (uint32_t)(hend - P));  // <= 43 + 15 since the drain
