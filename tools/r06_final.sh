@@ -4,7 +4,8 @@
 #   part 1: pytest -m gpu, smoke(), the default bench line (driver command),
 #           rocprofv3 --kernel-trace --stats of the Large line with its timed
 #           steps cut out (tools/timed_stats.py)
-#   part 2: the same for the Small line, and the zero-copy leg's trace
+#   part 2: the same for the Small line (pipelined and --serial), and the
+#           zero-copy leg's trace
 set -u
 out=$1; part=$2
 mkdir -p $out
@@ -30,6 +31,9 @@ if [ "$part" = 1 ]; then
 fi
 if [ "$part" = 2 ]; then
   trace small --shape small --steps 20 --warmup 5 $NL || exit 1
+  # the same with one stream (no copy beside the metadata kernels): how much
+  # the pipeline stretches each metadata kernel
+  trace small_serial --shape small --serial --steps 20 --warmup 5 $NL || exit 3
   timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $out/prof_zc -o run --output-format csv \
     -- python3 bench.py --mode decode --decode-leg zero_copy --zc-forms default --steps 10 --no-cpu-baseline \
     --no-host-path --legs none > $out/bench_prof_zc.json 2> $out/prof_zc.log || exit 2
