@@ -43,6 +43,9 @@ constexpr uint64_t NOWIN = ~0ull;
 // Where a window starts: the 16-byte block holding the walk's position, or
 // (HONU_WIN_ALIGN 64 / 128, an A/B build) the memory unit holding it, so
 // that a window never ends inside a unit the next refill fetches again.
+#ifndef HONU_GATHER_SKIP_WIN
+#define HONU_GATHER_SKIP_WIN 0
+#endif
 #ifndef HONU_WIN_ALIGN
 #define HONU_WIN_ALIGN 16
 #endif
@@ -488,9 +491,26 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
     }
     uint64_t ak = 0;
     const bool spec_acl = early.spec_acl;  // wave-uniform
-    if (!spec_acl && __ballot(fast)) {
-        const uint64_t gbase = fast ? acl_pos : 0;
-        const uint32_t gcnt = fast ? (uint32_t)(nacl < 64 ? nacl : 64) : 0;
+    // HONU_GATHER_SKIP_WIN 1: the flags the lane's window already holds (the
+    // list's start, <= 15 entries) are checked from LDS first and the burst
+    // gathers only the ones after them, so it does not fetch the window's
+    // lines a second time.
+    uint32_t a0 = 0;
+#if HONU_GATHER_SKIP_WIN
+    if (!spec_acl && fast && W.in(acl_pos)) {
+        const uint64_t room = (W.wb + WB - acl_pos + 17) / 18;
+        a0 = (uint32_t)(nacl < room ? nacl : room);
+        bool ok = true;
+#pragma unroll
+        for (uint32_t j = 0; j < (WB + 17) / 18; j++)
+            if (j < a0) ok &= W.at(acl_pos + 18ull * j) == 1;
+        if (!ok) fast = false;  // the entries are walked one by one below
+        ak = fast ? a0 : 0;
+    }
+#endif
+    if (!spec_acl && __ballot(fast && ak < nacl)) {
+        const uint64_t gbase = fast ? acl_pos + 18ull * a0 : 0;
+        const uint32_t gcnt = fast ? (uint32_t)(nacl - a0 < 64 ? nacl - a0 : 64) : 0;
         wave_sync();  // the windows' last reads are done
 #pragma unroll 4
         for (uint32_t k = 0; k < HONU_WAVE; k++) {
@@ -504,14 +524,14 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
         wave_sync();
         W.wb = NOWIN;  // the windows' bytes are gone
         if (fast) {
-            const uint32_t m = (uint32_t)(nacl < 64 ? nacl : 64);
+            const uint32_t m = gcnt;
             const __attribute__((address_space(3))) uint8_t *fl =
                 (const __attribute__((address_space(3))) uint8_t *)(W.wave + FLAG_ROW * lane);
             bool ok = true;
 #pragma unroll
             for (uint32_t j = 0; j < 64; j++)
-                if (j < m) ok &= fl[4 * j + (uint32_t)((acl_pos + 18ull * j) & 3)] == 1;
-            ak = m;
+                if (j < m) ok &= fl[4 * j + (uint32_t)((gbase + 18ull * j) & 3)] == 1;
+            ak = a0 + m;
             if (!ok) fast = false;  // the entries are walked one by one below
         }
         wave_sync();  // the gather area becomes windows again
