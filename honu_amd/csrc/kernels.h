@@ -26,7 +26,11 @@ struct DecodeScratch {
 // parses for the group fill (positions are < 2^62).
 #define GRP_ACL_FAST (1ull << 63)    // acl_pos: every entry present, entry j at acl_pos + 18 j
 #define GRP_REG_INLINE (1ull << 62)  // regions_pos: region ids in reg_inline[8 i ..]
-#define GRP_POS_MASK (~(GRP_ACL_FAST | GRP_REG_INLINE))
+// acl_pos bits 56-59 (GRP_ACL_FAST lists, HONU_GATHER_SKIP_WIN): how many of
+// the list's first flags the walk already checked from its window (win.h)
+#define GRP_ACL_A0_SHIFT 56
+#define GRP_ACL_A0(pos) (((pos) >> GRP_ACL_A0_SHIFT) & 15ull)
+#define GRP_POS_MASK ((1ull << GRP_ACL_A0_SHIFT) - 1)  // positions < 2^56
 // Flag on the lane encoder's ACL list position: every entry present, and the
 // list's partial end chunks are already written (the group kernel stores the
 // whole chunks in between).

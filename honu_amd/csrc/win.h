@@ -493,11 +493,13 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
     const bool spec_acl = early.spec_acl;  // wave-uniform
     // HONU_GATHER_SKIP_WIN 1: the flags the lane's window already holds (the
     // list's start, <= 15 entries) are checked from LDS first and the burst
-    // gathers only the ones after them, so it does not fetch the window's
-    // lines a second time.
+    // (here, or the speculative decode's after its publish: the count rides
+    // in acl_pos, GRP_ACL_A0) gathers only the ones after them, so it does
+    // not fetch the window's lines a second time. A flag that is not 1 here
+    // sends the list to the entry-by-entry walk below, speculative or not.
     uint32_t a0 = 0;
 #if HONU_GATHER_SKIP_WIN
-    if (!spec_acl && fast && W.in(acl_pos)) {
+    if (fast && W.in(acl_pos)) {
         const uint64_t room = (W.wb + WB - acl_pos + 17) / 18;
         a0 = (uint32_t)(nacl < room ? nacl : room);
         bool ok = true;
@@ -564,7 +566,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
                 pr |= HONU_ACL_INPLACE;
                 R.u64(OFF(acl_off), acl_pos);
             }
-            acl_pos |= GRP_ACL_FAST;  // for the fill
+            acl_pos |= GRP_ACL_FAST | ((uint64_t)a0 << GRP_ACL_A0_SHIFT);  // for the fill
         } else {
             for (uint64_t k = 0; k < nacl && st == HONU_OK; k++) {
                 STEP(D.boolean(f));
