@@ -26,7 +26,10 @@ trace() {  # name args...: kernel-trace + stats of one bench command, timed wind
 if [ "$part" = 1 ]; then
   timeout -k 10 900 python -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread tests > $out/gpu_suite.log 2>&1 || exit 1
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || exit 2
+  t0=$(date +%s.%N)
   timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > $out/bench_default.json 2> $out/bench_default.err || exit 3
+  t1=$(date +%s.%N)
+  python3 -c "print('bench.py --steps 20 --warmup 5 wall time: %.1f s' % ($t1 - $t0))" > $out/bench_default_wall.txt
   trace large $NL || exit 4
 fi
 if [ "$part" = 2 ]; then
