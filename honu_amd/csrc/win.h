@@ -40,14 +40,19 @@ constexpr uint32_t WSL = WB / 16 + 1;  // LDS stride in 16-byte slots: one pad s
                                        // on different banks
 constexpr uint32_t WS = WSL * 16;
 constexpr uint64_t NOWIN = ~0ull;
-// Where a window starts: the 16-byte block holding the walk's position, or
-// (HONU_WIN_ALIGN 64 / 128, an A/B build) the memory unit holding it, so
-// that a window never ends inside a unit the next refill fetches again.
+// Where a window starts: the 64-byte unit holding the walk's position, so
+// that a window ends on a unit boundary and the next refill does not fetch
+// its last line's rest again (16: the block; 128: the line, which leaves too
+// little of the window ahead, 1.5-4 % slower). HONU_GATHER_SKIP_WIN: below,
+// at the ACL flag burst. Both defaults measured in round 6
+// (profiles/r06/gather_skip/): the decode reads 1.625 -> 1.448 GB per 1M
+// records zero copy and 1.627 -> 1.461 GB materialising at equal time; the
+// line model (tools/decode_line_model.py) predicts both within 1 %.
 #ifndef HONU_GATHER_SKIP_WIN
-#define HONU_GATHER_SKIP_WIN 0
+#define HONU_GATHER_SKIP_WIN 1
 #endif
 #ifndef HONU_WIN_ALIGN
-#define HONU_WIN_ALIGN 16
+#define HONU_WIN_ALIGN 64
 #endif
 static_assert(HONU_WIN_ALIGN >= 16 && HONU_WIN_ALIGN <= 128 && (HONU_WIN_ALIGN & (HONU_WIN_ALIGN - 1)) == 0,
               "a power of two from a block to half the window");
