@@ -53,6 +53,10 @@ def parse_args(argv=None):
                    help="ranks (one per GPU); without torchrun the ranks are spawned here")
     p.add_argument("--dry-run", action="store_true",
                    help="stop before any device work: ranks report their shard (launcher test)")
+    p.add_argument("--shared-gpu", action="store_true",
+                   help="rehearsal of the N > 1 code paths on a one-GPU box: every rank on GPU 0, "
+                        "gloo instead of RCCL (the scatter staged through host memory); the "
+                        "numbers are not a measurement")
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--records", type=int, default=1 << 20, help="records per GPU")
@@ -1246,7 +1250,7 @@ def launch(args, argv):
     failing exit code. Nothing here touches the GPU (device_count() only
     counts), so the children own their devices from the start."""
     n = args.gpus
-    if not args.dry_run:
+    if not args.dry_run and not args.shared_gpu:
         visible = torch.cuda.device_count()
         if visible < n:
             print(f"bench.py: --gpus {n} needs {n} GPUs, {visible} visible", file=sys.stderr)
@@ -1303,6 +1307,8 @@ def main(argv=None):
     if args.dry_run:
         dry_run(args, world, rank)
         return
+    if args.shared_gpu:  # rehearsal: every rank on GPU 0 (gloo below)
+        local = 0
     if local >= torch.cuda.device_count():
         print(f"bench.py: rank {rank} needs GPU {local}, {torch.cuda.device_count()} visible",
               file=sys.stderr)
@@ -1311,7 +1317,10 @@ def main(argv=None):
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.shared_gpu:  # RCCL refuses two ranks on one device
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     def barrier():
         if dist is not None:
@@ -1435,6 +1444,7 @@ def gpu_parse_check(local):
     def check(mine, moff, cnt):
         c = Codec(local, max(cnt, 1))
         dev = torch.device("cuda", local)
+        mine, moff = mine.to(dev), moff.to(dev)  # (gloo: received in host memory)
         rows = torch.empty(352 * max(cnt, 1), dtype=torch.uint8, device=dev)
         info = torch.empty(32 * max(cnt, 1), dtype=torch.uint8, device=dev)
         s = torch.cuda.current_stream(dev).cuda_stream
@@ -1741,6 +1751,8 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
             a, b, sl = bench.zc_chunk
             off = sl.out_off.view(torch.int64)[: b - a + 1]
             arena = sl.out[: int(off[b - a].item())]
+            if dist.get_backend() != "nccl":  # gloo moves host tensors only
+                arena, off = arena.cpu(), off.cpu()
         scatter = scatter_leg(arena, off, dist, world, all_ok, gpu_parse_check(local),
                               torch.cuda.synchronize)
     bench.release()

@@ -70,3 +70,25 @@ def test_default_line_legs():
     # only, XLarge encode + decode of 1/16 the records (64 K) + its zero copy
     assert bench.LEG_SHAPES == {"small": ("small", False, 1, False), "mixed_encode": ("mixed", True, 1, False),
                                 "medium": ("medium", False, 1, False), "xlarge": ("xlarge", False, 1 / 16, True)}
+
+
+@pytest.mark.gpu
+def test_two_ranks_rehearsal_on_one_gpu():
+    """The N > 1 branch of the line (barriers, max over ranks, the all-ranks
+    totals, the scatter leg and its per-rank parse, the decode legs'
+    aggregates) run end to end by two ranks on one GPU (--shared-gpu: gloo
+    instead of RCCL, which refuses two ranks on one device); every rank's
+    records verified. The timing is not a measurement."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    r = _run(["--gpus", "2", "--shared-gpu", "--shape", "small", "--records", "8192", "--steps", "2",
+              "--warmup", "1", "--no-cpu-baseline", "--no-host-path", "--legs", "none"], timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["verified"] is True
+    assert out["config"]["records_per_gpu"] == 8192
+    assert out["scatter"]["verified"] is True and out["scatter"]["bytes_sent_by_rank0"] > 0
+    assert out["decode"]["verified"] is True and out["decode"]["all_ranks"]["ranks"] == 2
