@@ -249,7 +249,7 @@ HONU_DEV void flag_gather(uint8_t *ws, const uint8_t *__restrict__ rec, uint64_t
         if (lane < mk)
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)(rec + ((bk + 18ull * lane) & ~3ull)),
-                (__attribute__((address_space(3))) void *)(ws + FLAG_ROW * k), 4, 0, 0);
+                (__attribute__((address_space(3))) void *)(ws + FLAG_ROW * k), 4, 0, HONU_BURST_AUX);
     }
 }
 // After flag_gather(.., 0): true when a flag of this lane's list (chk) is not

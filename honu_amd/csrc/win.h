@@ -48,6 +48,14 @@ constexpr uint64_t NOWIN = ~0ull;
 // (profiles/r06/gather_skip/): the decode reads 1.625 -> 1.448 GB per 1M
 // records zero copy and 1.627 -> 1.461 GB materialising at equal time; the
 // line model (tools/decode_line_model.py) predicts both within 1 %.
+// Cache policy of the window refills and of the ACL flag bursts (the aux
+// operand of global_load_lds; 2 = nt, an A/B build): 0, the default policy.
+#ifndef HONU_WIN_AUX
+#define HONU_WIN_AUX 0
+#endif
+#ifndef HONU_BURST_AUX
+#define HONU_BURST_AUX 0
+#endif
 #ifndef HONU_GATHER_SKIP_WIN
 #define HONU_GATHER_SKIP_WIN 1
 #endif
@@ -112,7 +120,7 @@ struct LaneWin {
                 if (!held && 16 * blk < lims[L])
                     __builtin_amdgcn_global_load_lds(
                         (const __attribute__((address_space(1))) void *)(rec + 16 * blk),
-                        (__attribute__((address_space(3))) void *)(wave + 1024 * k), 16, 0, 0);
+                        (__attribute__((address_space(3))) void *)(wave + 1024 * k), 16, 0, HONU_WIN_AUX);
             }
         }
         __builtin_amdgcn_s_waitcnt(0);
@@ -525,7 +533,7 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
             if (lane < __builtin_amdgcn_readlane(gcnt, k))
                 __builtin_amdgcn_global_load_lds(
                     (const __attribute__((address_space(1))) void *)(rec + ((base + 18ull * lane) & ~3ull)),
-                    (__attribute__((address_space(3))) void *)(W.wave + FLAG_ROW * k), 4, 0, 0);
+                    (__attribute__((address_space(3))) void *)(W.wave + FLAG_ROW * k), 4, 0, HONU_BURST_AUX);
         }
         __builtin_amdgcn_s_waitcnt(0);
         wave_sync();
