@@ -437,7 +437,8 @@ int32_t honu_decode_payloads(honu_ctx *ctx, const uint8_t *d_rec, uint64_t n,
  * by the table fill or a gather after the publish) when the param
  * "speculate" allows it — by default materialising calls and the table forms,
  * not a zero-copy call with both lists in place; a batch holding any record that fails after its counts
- * were published, or a nil ACL entry, is decoded a second time without
+ * were published, or a nil ACL entry past the list's first bytes (those the
+ * walk has at hand are checked at once), is decoded a second time without
  * speculation inside the same call, so such a batch costs about twice a
  * clean one (malformed input and nil entries only; results are exact either
  * way). A recovery that ran sets a pinned word of the context, and the
