@@ -469,12 +469,13 @@ HONU_DEV void decode_fused_body(
         // round trip hides under the wait and no table bytes are written.
         // (The two forms never stage at once: an in-place list has ntab 0.)
         // (the first GRP_ACL_A0 flags the walk checked from its window)
+        // (and its last GRP_ACL_TL, from the window after the list)
         const bool ichk = INPL && early.spec_acl && valid && P.st == HONU_OK &&
-                          P.nacl > GRP_ACL_A0(P.acl_pos) && (P.acl_pos & GRP_ACL_FAST);
+                          P.nacl > GRP_ACL_A0(P.acl_pos) + GRP_ACL_TL(P.acl_pos) && (P.acl_pos & GRP_ACL_FAST);
         const bool igather = INPL && early.spec_acl && __ballot(ichk);  // wave-uniform
         if (igather)
             flag_gather(ws, rec, ichk ? (P.acl_pos & GRP_POS_MASK) + 18 * GRP_ACL_A0(P.acl_pos) : 0,
-                        ichk ? P.nacl - GRP_ACL_A0(P.acl_pos) : 0, 0);
+                        ichk ? P.nacl - GRP_ACL_A0(P.acl_pos) - GRP_ACL_TL(P.acl_pos) : 0, 0);
         WSTAMP(10);  // publish + rows out + first staging round issued
 #if defined(HONU_STAGE_TIMING) && defined(HONU_STAGE_DRAIN)
         // (timing variant: the wave's outstanding stores and loads drained
@@ -594,7 +595,7 @@ HONU_DEV void decode_fused_body(
         WSTAMP(12);  // info, regions, lists with nil entries
         if (igather)
             acl_bad |= flag_check(ws, rec, ichk, (P.acl_pos & GRP_POS_MASK) + 18 * GRP_ACL_A0(P.acl_pos),
-                                  P.nacl - GRP_ACL_A0(P.acl_pos));
+                                  P.nacl - GRP_ACL_A0(P.acl_pos) - GRP_ACL_TL(P.acl_pos));
         // staged lists: round by round, lane e of a pass takes entry e of the
         // round's entries (one run of the table per record), reads its 17
         // bytes from LDS and stores the 20-byte row

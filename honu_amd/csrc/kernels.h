@@ -30,7 +30,11 @@ struct DecodeScratch {
 // the list's first flags the walk already checked from its window (win.h)
 #define GRP_ACL_A0_SHIFT 56
 #define GRP_ACL_A0(pos) (((pos) >> GRP_ACL_A0_SHIFT) & 15ull)
-#define GRP_POS_MASK ((1ull << GRP_ACL_A0_SHIFT) - 1)  // positions < 2^56
+// bits 53-55 (HONU_GATHER_SKIP_WIN2): how many of its last flags it checked
+// from the window after the list
+#define GRP_ACL_TL_SHIFT 53
+#define GRP_ACL_TL(pos) (((pos) >> GRP_ACL_TL_SHIFT) & 7ull)
+#define GRP_POS_MASK ((1ull << GRP_ACL_TL_SHIFT) - 1)  // positions < 2^53
 // Flag on the lane encoder's ACL list position: every entry present, and the
 // list's partial end chunks are already written (the group kernel stores the
 // whole chunks in between).

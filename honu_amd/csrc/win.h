@@ -63,6 +63,9 @@ constexpr uint64_t NOWIN = ~0ull;
 #ifndef HONU_GATHER_SKIP_WIN
 #define HONU_GATHER_SKIP_WIN 1
 #endif
+#ifndef HONU_GATHER_SKIP_WIN2
+#define HONU_GATHER_SKIP_WIN2 0
+#endif
 #ifndef HONU_WIN_ALIGN
 #define HONU_WIN_ALIGN 64
 #endif
@@ -529,9 +532,23 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
         ak = fast ? a0 : 0;
     }
 #endif
-    if (!spec_acl && __ballot(fast && ak < nacl)) {
+    // HONU_GATHER_SKIP_WIN2 1: likewise the list's last flags (<= 4) that
+    // window 2, placed at the list's end, will hold: checked from it after its
+    // refill (a flag that is not 1 there reverts the list to the
+    // entry-by-entry walk), their count riding in acl_pos (GRP_ACL_TL).
+    uint32_t tl = 0;
+#if HONU_GATHER_SKIP_WIN2
+    if (fast) {
+        const uint64_t w2b = win_base(acl_pos + 18 * nacl);
+        uint64_t jb = w2b > acl_pos ? (w2b - acl_pos + 17) / 18 : 0;  // the first flag at >= w2b
+        if (jb < a0) jb = a0;
+        tl = (uint32_t)(jb < nacl ? nacl - jb : 0);
+    }
+#endif
+    const uint64_t nhead = nacl - tl;  // the flags checked before window 2
+    if (!spec_acl && __ballot(fast && ak < nhead)) {
         const uint64_t gbase = fast ? acl_pos + 18ull * a0 : 0;
-        const uint32_t gcnt = fast ? (uint32_t)(nacl - a0 < 64 ? nacl - a0 : 64) : 0;
+        const uint32_t gcnt = fast ? (uint32_t)(nhead - a0 < 64 ? nhead - a0 : 64) : 0;
         wave_sync();  // the windows' last reads are done
 #pragma unroll 4
         for (uint32_t k = 0; k < HONU_WAVE; k++) {
@@ -558,21 +575,21 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
         wave_sync();  // the gather area becomes windows again
     }
     if (!spec_acl) {
-        bool chk = fast && ak < nacl;
+        bool chk = fast && ak < nhead;
         while (__ballot(chk)) {
             W.refill(chk ? win_base(D.p + 18 * ak) : NOWIN);
             if (chk) {
                 // the flags this window holds (at most 15), read independently
                 const uint64_t q = D.p + 18 * ak;
                 const uint64_t room = W.in(q) ? (W.wb + WB - q + 17) / 18 : 0;
-                const uint32_t cnt = (uint32_t)(nacl - ak < room ? nacl - ak : room);
+                const uint32_t cnt = (uint32_t)(nhead - ak < room ? nhead - ak : room);
                 bool ok = true;
 #pragma unroll
                 for (uint32_t j = 0; j < (WB + 17) / 18; j++)
                     if (j < cnt) ok &= W.at(q + 18 * j) == 1;
                 ak += cnt;
                 if (!ok) fast = false;  // the entries are walked one by one below
-                if (!fast || ak == nacl) chk = false;
+                if (!fast || ak == nhead) chk = false;
             }
         }
     }
@@ -585,7 +602,8 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
                 pr |= HONU_ACL_INPLACE;
                 R.u64(OFF(acl_off), acl_pos);
             }
-            acl_pos |= GRP_ACL_FAST | ((uint64_t)a0 << GRP_ACL_A0_SHIFT);  // for the fill
+            acl_pos |= GRP_ACL_FAST | ((uint64_t)a0 << GRP_ACL_A0_SHIFT) |
+                       ((uint64_t)tl << GRP_ACL_TL_SHIFT);  // for the fill
         } else {
             for (uint64_t k = 0; k < nacl && st == HONU_OK; k++) {
                 STEP(D.boolean(f));
@@ -596,10 +614,33 @@ HONU_DEV void win_walk(uint64_t i0, uint8_t *wave_smem, const uint8_t *__restric
             }
         }
     }
-    if (hm) R.u64(OFF(acl_count), nacl);  // 0 for an empty list (metadata.go:254)
     WSTAMP(5);  // ACL flags checked
     W.refill(hm && st == HONU_OK ? win_base(D.p) : NOWIN);
     WSTAMP(6);  // window after the list
+#if HONU_GATHER_SKIP_WIN2
+    if (fast && tl) {  // the last flags, from window 2 (or memory, W.u8)
+        const uint64_t ap = acl_pos & GRP_POS_MASK;
+        bool ok = true;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++)
+            if (j < tl) ok &= W.u8(ap + 18 * (nacl - tl + j)) == 1;
+        if (!ok) {  // a nil entry among them: the list is walked entry by entry after all
+            fast = false;
+            inpl = false;
+            pr &= ~(uint32_t)HONU_ACL_INPLACE;
+            acl_pos = ap;
+            D.p = ap;
+            for (uint64_t k = 0; k < nacl && st == HONU_OK; k++) {
+                STEP(D.boolean(f));
+                if (st == HONU_OK && f) {
+                    STEP(D.ulid(lo, hi));
+                    STEP(D.u8(u));
+                }
+            }
+        }
+    }
+#endif
+    if (hm) R.u64(OFF(acl_count), nacl);  // 0 for an empty list (metadata.go:254)
     if (hm) {
         STEP(D.u64(nreg));                                  // region.go:154-169
         if (st == HONU_OK && nreg > GO_MAX_ALLOC / 4) st = HONU_ERR_PANIC;  // make(Regions, n)

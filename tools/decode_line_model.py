@@ -10,7 +10,10 @@ its lines again: the L2 kept nothing between phases), `union` once per record
 (perfect reuse); the measured read bytes per record (PMC, 1.625 GB / 1M) lie
 between them, near `sum`. Pairwise overlaps name the lines fetched twice.
 
-  python tools/decode_line_model.py [--n 4000] [--skip-window-flags] [--align 16]
+  python tools/decode_line_model.py [--n 4000] [--align 64] [--skip-window-flags] [--skip-window2-flags]
+
+(The model has no cache: the nt policy of the window refills and bursts,
+which lets the L2 keep the tile head's lines, is outside it.)
 """
 import argparse
 import itertools
@@ -41,6 +44,8 @@ def main():
     ap.add_argument("--align", type=int, default=16, help="window base alignment (HONU_WIN_ALIGN)")
     ap.add_argument("--skip-window-flags", action="store_true",
                     help="the burst skips the flags window 1 holds (HONU_GATHER_SKIP_WIN)")
+    ap.add_argument("--skip-window2-flags", action="store_true",
+                    help="... and the last ones window 2 holds (HONU_GATHER_SKIP_WIN2)")
     a = ap.parse_args()
     from oracle import oracle as O
     from honu_amd.workload import gen_host_batch
@@ -58,7 +63,7 @@ def main():
         tstart = int(inf["data_off"]) + int(inf["data_len"]) if int(inf["data_len"]) else beg + 2
         S = {}
         A = beg & ~15
-        S["head"] = lines(A, A + 16) | (lines(A + 16, A + 32) if (beg & 15) and A + 16 < end else set())
+        S["head"] = lines(A, A + 16) | (lines(A + 16, A + 32) if (beg & 15) > 5 and A + 16 < end else set())
         w1 = base(tstart)
         S["w1"] = lines(w1, min(w1 + 256, end))
         na, ap_ = int(m["acl_count"]), int(m["acl_off"])
@@ -67,7 +72,11 @@ def main():
             j0 = 0
             if a.skip_window_flags and ap_ < w1 + 256:
                 j0 = min(na, (w1 + 256 - ap_ + 17) // 18)
-            for j in range(j0, min(na, j0 + 64)):
+            j1 = na
+            if a.skip_window2_flags:
+                w2b = base(ap_ + 18 * na)
+                j1 = max(j0, min(na, (w2b - ap_ + 17) // 18)) if w2b > ap_ else j0
+            for j in range(j0, min(j1, j0 + 64)):
                 q = (ap_ + 18 * j) & ~3
                 S["acl"] |= lines(q, q + 4)
             p2 = ap_ + 18 * na
