@@ -55,6 +55,50 @@ def _speculative(c):
     hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"speculate", 1), "param")
 
 
+def _nil_at(metas, datas, k, where):
+    """k (meta, data) pairs from the random corpus whose ACL list is 40
+    entries long with nil entries at the positions `where`. Mid-list nils
+    (20) are only seen by the flag burst, so a speculative launch
+    misspeculates on them; nils among the first entries (the walk's window
+    holds them) or the last few (the window after the list) are caught by the
+    walk itself (win.h HONU_GATHER_SKIP_WIN / _WIN2)."""
+    from dataclasses import replace
+    from honu_amd.metadata import AccessControl
+    out = []
+    for m, d in zip(metas, datas):
+        if len(out) == k:
+            break
+        if not (m.ACL and d):
+            continue
+        base = [a for a in m.ACL if a is not None] or [AccessControl(bytes(range(16)), 3)]
+        acl = (base * 40)[:40]
+        for w in where:
+            acl[w] = None
+        out.append((replace(m, ACL=acl), d))
+    assert len(out) == k
+    return out
+
+
+def _splice(oracle_lib, rec, off, pairs, first):
+    """rec/off of a batch with the encoded `pairs` replacing records spread
+    evenly from index `first` on."""
+    from honu_amd.metadata import pack_batch
+    n = len(off) - 1
+    r2, o2, st2 = oracle_lib.marshal_batch(pack_batch([m for m, _ in pairs], [d for _, d in pairs]))
+    assert (st2 == 0).all()
+    at = set(int(x) for x in np.linspace(first, n - 1, len(pairs)).astype(np.int64))
+    pieces, noff, j = [], [0], 0
+    for i in range(n):
+        if i in at:
+            r = r2[int(o2[j]):int(o2[j + 1])]
+            j += 1
+        else:
+            r = rec[int(off[i]):int(off[i + 1])]
+        pieces.append(r)
+        noff.append(noff[-1] + len(r))
+    return np.concatenate(pieces), np.array(noff, np.uint64)
+
+
 def _dev(a, codec):
     return hobj._dev_bytes(np.ascontiguousarray(a), codec.torch_device)
 
@@ -243,26 +287,9 @@ def test_speculative_acl_flags_recover(oracle_lib, n, k, inplace, inline_rec, gu
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from corpora import random_metas
-    from honu_amd.metadata import pack_batch
     rec, off, _ = oracle_lib.marshal_batch(gen_host_batch(43, "small", 0, n))
     metas, datas = random_metas(4 * k + 40, 77)
-    pick = [i for i, m in enumerate(metas)
-            if m.ACL and any(a is None for a in m.ACL) and datas[i]][:k]
-    assert len(pick) == k
-    r2, o2, st2 = oracle_lib.marshal_batch(pack_batch([metas[i] for i in pick],
-                                                      [datas[i] for i in pick]))
-    assert (st2 == 0).all()
-    at = set(int(x) for x in np.linspace(3, n - 1, k).astype(np.int64))
-    pieces, noff, j = [], [0], 0
-    for i in range(n):
-        if i in at:
-            r = r2[int(o2[j]):int(o2[j + 1])]
-            j += 1
-        else:
-            r = rec[int(off[i]):int(off[i + 1])]
-        pieces.append(r)
-        noff.append(noff[-1] + len(r))
-    brec, boff = np.concatenate(pieces), np.array(noff, np.uint64)
+    brec, boff = _splice(oracle_lib, rec, off, _nil_at(metas, datas, k, [20]), 3)
     c = hobj.Codec(0, n)
     try:
         _speculative(c)
@@ -441,23 +468,10 @@ def test_speculate_auto(oracle_lib, inplace):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from corpora import random_metas
-    from honu_amd.metadata import pack_batch
     n = 140000
     rec, off, _ = oracle_lib.marshal_batch(gen_host_batch(47, "small", 0, n))
     metas, datas = random_metas(200, 79)
-    pick = [i for i, m in enumerate(metas) if m.ACL and any(a is None for a in m.ACL) and datas[i]][:20]
-    r2, o2, _ = oracle_lib.marshal_batch(pack_batch([metas[i] for i in pick], [datas[i] for i in pick]))
-    at = set(int(x) for x in np.linspace(5, n - 1, len(pick)).astype(np.int64))
-    pieces, noff, j = [], [0], 0
-    for i in range(n):
-        if i in at:
-            r = r2[int(o2[j]):int(o2[j + 1])]
-            j += 1
-        else:
-            r = rec[int(off[i]):int(off[i + 1])]
-        pieces.append(r)
-        noff.append(noff[-1] + len(r))
-    brec, boff = np.concatenate(pieces), np.array(noff, np.uint64)
+    brec, boff = _splice(oracle_lib, rec, off, _nil_at(metas, datas, 20, [20]), 5)
     c = hobj.Codec(0, n)
     try:
         hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
@@ -472,3 +486,97 @@ def test_speculate_auto(oracle_lib, inplace):
         assert _get(c, b"recoveries") == r0 + (0 if inplace == 1 else 1)
     finally:
         c.close()
+
+
+def _caught(t, prefix, na, first):
+    """Whether the walk itself sees a list's first nil entry (index `first`)
+    without the flag burst (win.h): window 1, [t & ~63, +256) from the tail's
+    start t, holds the first flags (a0); the window after the speculated list
+    end E, from E's 64-byte unit on, its last ones (tl). prefix: the tail's
+    bytes before the list, na: its entries."""
+    ap = t + prefix
+    w1 = t & ~63
+    a0 = min(na, (w1 + 256 - ap + 17) // 18) if w1 <= ap < w1 + 256 else 0
+    w2 = (ap + 18 * na) & ~63
+    jb = max(a0, min(na, (w2 - ap + 17) // 18) if w2 > ap else 0)
+    tl = na - jb if jb < na else 0
+    return first < a0 or first >= na - tl
+
+
+def _placed_batch(oracle_lib, rec, off, pairs, twins, first, want, every=2311):
+    """The batch rec/off with the nil-entry records `pairs` spliced in every
+    `every` records, each one's payload lengthened by 0-63 bytes so that its
+    tail starts where _caught(...) == want (the geometry the walk sees)."""
+    from honu_amd.metadata import pack_batch
+    r2, o2, _ = oracle_lib.marshal_batch(pack_batch([m for m, _ in twins], [d for _, d in twins]))
+    meta, info = oracle_lib.decode_batch(r2, o2)[:2]
+    geo = [(int(meta[j]["acl_off"]) - int(info[j]["data_off"]) - int(info[j]["data_len"]),
+            int(meta[j]["acl_count"])) for j in range(len(twins))]
+    n = len(off) - 1
+    pieces, noff, k, placed = [], [0], 0, 0
+    for i in range(n):
+        r = None
+        if i % every == 7 and k < len(pairs):
+            (m, d), (prefix, na) = pairs[k], geo[k]
+            k += 1
+            for delta in range(64):
+                dl = len(d) + delta
+                t = noff[-1] + 1 + len(_uvarint(dl)) + dl
+                if _caught(t, prefix, na, first) == want:
+                    d2 = (d * (dl // len(d) + 1))[:dl]
+                    rr, oo, st = oracle_lib.marshal_batch(pack_batch([m], [d2]))
+                    assert st[0] == 0
+                    r = rr[:int(oo[1])]
+                    placed += 1
+                    break
+        if r is None:
+            r = rec[int(off[i]):int(off[i + 1])]
+        pieces.append(r)
+        noff.append(noff[-1] + len(r))
+    return np.concatenate(pieces), np.array(noff, np.uint64), placed
+
+
+def _uvarint(x):
+    out = bytearray()
+    while x >= 0x80:
+        out.append((x & 0x7F) | 0x80)
+        x >>= 7
+    out.append(x)
+    return bytes(out)
+
+
+@FORMS
+@pytest.mark.parametrize("where", [[0], [1, 12], [39], [37, 38], [0, 39], [20]],
+                         ids=["first", "window", "last", "tail", "both_ends", "middle"])
+def test_walk_catches_nil_entries_at_the_list_ends(oracle_lib, where, inplace):
+    """Nil ACL entries the walk sees itself — among the first flags, which the
+    window at the tail's start holds, or the last few, which the window after
+    the list holds (win.h HONU_GATHER_SKIP_WIN / _WIN2) — send the list to
+    the entry-by-entry walk at once: a speculative 2188-tile batch holding
+    such records (placed so that the windows hold their first nil: _caught)
+    decodes bit-exact with no recovery launch; with records whose first nil
+    (index 20) only the flag burst sees, the batch recovers once. Without
+    speculation: bit-exact, never a recovery."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from corpora import random_metas
+    n = 140000
+    rec, off, _ = oracle_lib.marshal_batch(gen_host_batch(49, "small", 0, n))
+    metas, datas = random_metas(120, 81)
+    walk = where != [20]
+    pairs = _nil_at(metas, datas, 40, where)
+    twins = _nil_at(metas, datas, 40, [])  # the same records, every entry present
+    brec, boff, placed = _placed_batch(oracle_lib, rec, off, pairs, twins, min(where), walk)
+    assert placed >= 8
+    for spec in (1, 0):
+        c = hobj.Codec(0, n)
+        try:
+            hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"record_variant", 6), "param")
+            hobj._lib.check(c.lib.honu_ctx_set_param(c.ctx, b"speculate", spec), "param")
+            r0 = _get(c, b"recoveries")
+            d = _Dec(c, brec, boff, inplace)
+            assert d() == 0
+            d.check(oracle_lib, brec, boff)
+            assert _get(c, b"recoveries") == r0 + (1 if spec and not walk else 0)
+        finally:
+            c.close()
