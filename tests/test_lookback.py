@@ -74,7 +74,10 @@ def _nil_at(metas, datas, k, where):
         acl = (base * 40)[:40]
         for w in where:
             acl[w] = None
-        out.append((replace(m, ACL=acl), d))
+        # six 5-byte region ids after the list: the record holds the 18 bytes
+        # per entry a speculated list takes (17 more than a nil's 1), so the
+        # list is speculated, not walked for want of room
+        out.append((replace(m, ACL=acl, WriteRegions=[(1 << 28) + r for r in range(6)]), d))
     assert len(out) == k
     return out
 
