@@ -61,7 +61,9 @@ def _nil_at(metas, datas, k, where):
     (20) are only seen by the flag burst, so a speculative launch
     misspeculates on them; nils among the first entries (the walk's window
     holds them) or the last few (the window after the list) are caught by the
-    walk itself (win.h HONU_GATHER_SKIP_WIN / _WIN2)."""
+    walk itself (win.h HONU_GATHER_SKIP_WIN / _WIN2). (Any byte other than 1
+    where the walk looks for a flag sends the list to the entry-by-entry walk,
+    which is exact either way.)"""
     from dataclasses import replace
     from honu_amd.metadata import AccessControl
     out = []
@@ -70,7 +72,12 @@ def _nil_at(metas, datas, k, where):
             break
         if not (m.ACL and d):
             continue
-        base = [a for a in m.ACL if a is not None] or [AccessControl(bytes(range(16)), 3)]
+        # Permissions 1 everywhere: after a nil entry, the speculated flag
+        # positions of the later entries hold their Permissions bytes, so the
+        # walk's look at the last flags passes and only the burst sees a
+        # mid-list nil
+        base = [AccessControl(a.ClientID, 1) for a in m.ACL if a is not None] or \
+            [AccessControl(bytes(range(16)), 1)]
         acl = (base * 40)[:40]
         for w in where:
             acl[w] = None
