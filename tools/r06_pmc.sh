@@ -31,6 +31,12 @@ if [ "$part" = 1 ]; then
     --mode decode --decode-leg materialising --no-cpu-baseline --no-host-path --legs none || exit 3
   run pmc_small "1048576 small records per GPU: $ED" --shape small $NL || exit 4
 fi
+if [ "$part" = 3 ]; then  # the decode legs only (the kernels a decode-only change touches)
+  run pmc_zc "1048576 large records per GPU: decode (Object.Metadata + Object.Data) of one resident records arena, zero_copy" \
+    --mode decode --decode-leg zero_copy --zc-forms default --no-cpu-baseline --no-host-path --legs none || exit 2
+  run pmc_mat "1048576 large records per GPU: decode (Object.Metadata + Object.Data) of one resident records arena, materialising" \
+    --mode decode --decode-leg materialising --no-cpu-baseline --no-host-path --legs none || exit 3
+fi
 if [ "$part" = 2 ]; then
   run pmc_mixenc "1048576 mixed records per GPU: encode (object.Marshal)" --shape mixed --mode encode $NL || exit 1
   run pmc_medium "1048576 medium records per GPU: $ED" --shape medium $NL || exit 2
