@@ -375,6 +375,7 @@ int32_t honu_ctx_get_param(const honu_ctx *ctx, const char *name, int64_t *value
     else if (!strcmp(name, "copy_variant")) *value = ctx->geom.copy_variant;
     else if (!strcmp(name, "encode_variant")) *value = ctx->geom.encode_variant;
     else if (!strcmp(name, "record_variant")) *value = ctx->geom.record_variant;
+    else if (!strcmp(name, "walk_flag_checks")) *value = decode_walk_flag_checks();  // read only: the build's
     else return arg_fail(name);
     return HONU_OK;
 }

@@ -686,6 +686,12 @@ extern "C" int32_t honu_debug_stage_times(void *host, uint64_t waves, int32_t re
 }
 #endif
 
+// Which of a speculated list's entry flags the walk checks itself (win.h), as
+// this translation unit was built: bit 0 the first ones (window 1), bit 1 the
+// last ones (window 2). Read back as the context param "walk_flag_checks", so
+// tests know which nil entries cost a recovery launch.
+int decode_walk_flag_checks() { return (HONU_GATHER_SKIP_WIN ? 1 : 0) | (HONU_GATHER_SKIP_WIN2 ? 2 : 0); }
+
 hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                honu_meta *meta, honu_record_info *info, honu_acl *acl,
                                uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap, int materialize,

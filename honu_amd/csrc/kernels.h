@@ -173,6 +173,7 @@ hipError_t launch_decode_fill_grp(const uint8_t *rec, uint64_t n, honu_meta *met
 
 // fused.hip: one launch from records to rows, record info and tables
 // (materialize: also the data-arena offsets honu_decode_payloads copies to)
+int decode_walk_flag_checks();  // fused.hip: bit 0 window 1's flags, bit 1 window 2's
 hipError_t launch_decode_fused(const uint8_t *rec, const uint64_t *rec_off, uint64_t n,
                                honu_meta *meta, honu_record_info *info, honu_acl *acl,
                                uint64_t acl_cap, uint32_t *reg, uint64_t reg_cap, int materialize,

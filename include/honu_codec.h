@@ -299,7 +299,11 @@ int32_t honu_ctx_set_param(honu_ctx *ctx, const char *name, int64_t value);
 /* The current value of a parameter of honu_ctx_set_param, and
  * "speculate_backoff": how many of the context's next decode calls run
  * without speculation (16 once a recovery launch has run, see
- * honu_decode_records; the count drops by one per call). */
+ * honu_decode_records; the count drops by one per call), and
+ * "walk_flag_checks" (as built): which entry flags of a speculated ACL list
+ * the walk checks itself, so that a nil entry there costs no recovery launch —
+ * bit 0 the first ones (the window at the tail's start), bit 1 the last ones
+ * (the window after the list); the flags in between are the burst's. */
 int32_t honu_ctx_get_param(const honu_ctx *ctx, const char *name, int64_t *value);
 
 /* ABI self-description, used by bindings to check struct layouts. */

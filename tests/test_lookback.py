@@ -498,22 +498,24 @@ def test_speculate_auto(oracle_lib, inplace):
         c.close()
 
 
-def _caught(t, prefix, na, first):
+def _caught(t, prefix, na, first, checks=3):
     """Whether the walk itself sees a list's first nil entry (index `first`)
     without the flag burst (win.h): window 1, [t & ~63, +256) from the tail's
-    start t, holds the first flags (a0); the window after the speculated list
-    end E, from E's 64-byte unit on, its last ones (tl). prefix: the tail's
-    bytes before the list, na: its entries."""
+    start t, holds the first flags (a0; checks bit 0, HONU_GATHER_SKIP_WIN);
+    the window after the speculated list end E, from E's 64-byte unit on, its
+    last ones (tl; checks bit 1, HONU_GATHER_SKIP_WIN2). prefix: the tail's
+    bytes before the list, na: its entries. checks: the library's
+    "walk_flag_checks"."""
     ap = t + prefix
     w1 = t & ~63
-    a0 = min(na, (w1 + 256 - ap + 17) // 18) if w1 <= ap < w1 + 256 else 0
+    a0 = min(na, (w1 + 256 - ap + 17) // 18) if (checks & 1) and w1 <= ap < w1 + 256 else 0
     w2 = (ap + 18 * na) & ~63
     jb = max(a0, min(na, (w2 - ap + 17) // 18) if w2 > ap else 0)
-    tl = na - jb if jb < na else 0
+    tl = na - jb if (checks & 2) and jb < na else 0
     return first < a0 or first >= na - tl
 
 
-def _placed_batch(oracle_lib, rec, off, pairs, twins, first, want, every=2311):
+def _placed_batch(oracle_lib, rec, off, pairs, twins, first, want, checks, every=2311):
     """The batch rec/off with the nil-entry records `pairs` spliced in every
     `every` records, each one's payload lengthened by 0-63 bytes so that its
     tail starts where _caught(...) == want (the geometry the walk sees)."""
@@ -532,7 +534,7 @@ def _placed_batch(oracle_lib, rec, off, pairs, twins, first, want, every=2311):
             for delta in range(64):
                 dl = len(d) + delta
                 t = noff[-1] + 1 + len(_uvarint(dl)) + dl
-                if _caught(t, prefix, na, first) == want:
+                if _caught(t, prefix, na, first, checks) == want:
                     d2 = (d * (dl // len(d) + 1))[:dl]
                     rr, oo, st = oracle_lib.marshal_batch(pack_batch([m], [d2]))
                     assert st[0] == 0
@@ -573,10 +575,18 @@ def test_walk_catches_nil_entries_at_the_list_ends(oracle_lib, where, inplace):
     n = 140000
     rec, off, _ = oracle_lib.marshal_batch(gen_host_batch(49, "small", 0, n))
     metas, datas = random_metas(120, 81)
-    walk = where != [20]
+    c = hobj.Codec(0, 64)
+    try:
+        checks = _get(c, b"walk_flag_checks")  # which flags this build's walk checks itself
+    finally:
+        c.close()
+    # the walk sees the first nil: among the first flags (every case but the
+    # last-only and mid-list ones), or among the last ones when the build
+    # checks those from the window after the list
+    walk = (where[0] < 13 and bool(checks & 1)) or (where[0] > 36 and bool(checks & 2))
     pairs = _nil_at(metas, datas, 40, where)
     twins = _nil_at(metas, datas, 40, [])  # the same records, every entry present
-    brec, boff, placed = _placed_batch(oracle_lib, rec, off, pairs, twins, min(where), walk)
+    brec, boff, placed = _placed_batch(oracle_lib, rec, off, pairs, twins, min(where), walk, checks)
     assert placed >= 8
     for spec in (1, 0):
         c = hobj.Codec(0, n)
