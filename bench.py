@@ -118,6 +118,10 @@ def parse_args(argv=None):
                         "medium (1M Medium encode + decode), xlarge (--records/16 XLarge encode + "
                         "decode + chunk zero copy); auto: all four for the default Large line, none "
                         "otherwise; none: no legs")
+    p.add_argument("--legs-first", type=int, default=0, choices=[0, 1],
+                   help="1: run the legs before the main line (after the host path), each on a device "
+                        "the main line's ~250 GB of buffers have not yet been allocated and freed on; "
+                        "0: after the main line and the decode legs")
     p.add_argument("--leg-pause", type=float, default=0.0,
                    help="seconds the device idles before each leg (a probe of whether a leg's time "
                         "depends on the load before it; 0: none)")
@@ -1695,6 +1699,9 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
     # instead of 46 for Large records)
     host_path = None if args.no_host_path else host_path_leg(
         _Estimate(args, rank, world), args, local, world, gather_max, all_ok)
+    legs = None
+    if args.legs_first:
+        legs = run_legs(args, rank, local, world, dist, barrier, gather_max, all_ok)
     gc.collect()
     torch.cuda.empty_cache()
     bench = Bench(args, rank, local)
@@ -1758,7 +1765,8 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
     bench.release()
     decode = None if args.no_decode_legs else decode_legs(bench, args, world, barrier, gather_max,
                                                           all_ok)
-    legs = run_legs(args, rank, local, world, dist, barrier, gather_max, all_ok)
+    if not args.legs_first:
+        legs = run_legs(args, rank, local, world, dist, barrier, gather_max, all_ok)
     if rank != 0:
         return None
     if decode is not None and decode.get("materialising") is not None:  # the copy's achievable rate too
@@ -1854,6 +1862,7 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
         "verified_scope": None if ok_all is None else Bench.VERIFIED_SCOPE,
         "decode": decode,
         "legs": legs,
+        "legs_order": "before the main line" if args.legs_first else "after the main line and the decode legs",
         "host_path": host_path,
         "scatter": scatter,
     }
