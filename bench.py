@@ -118,10 +118,13 @@ def parse_args(argv=None):
                         "medium (1M Medium encode + decode), xlarge (--records/16 XLarge encode + "
                         "decode + chunk zero copy); auto: all four for the default Large line, none "
                         "otherwise; none: no legs")
-    p.add_argument("--legs-first", type=int, default=0, choices=[0, 1],
-                   help="1: run the legs before the main line (after the host path), each on a device "
-                        "the main line's ~250 GB of buffers have not yet been allocated and freed on; "
-                        "0: after the main line and the decode legs")
+    p.add_argument("--legs-at", choices=["first", "after_main", "end"], default="end",
+                   help="when the shape legs run: first (before the main line, after the host path), "
+                        "after_main (right after the main line, before the decode legs and their 207 GB "
+                        "records arena) or end (after the decode legs)")
+    p.add_argument("--host-path-at", choices=["first", "end"], default="first",
+                   help="when the host-path leg runs: first (on a device nothing else has touched yet) "
+                        "or end (after every other leg)")
     p.add_argument("--leg-pause", type=float, default=0.0,
                    help="seconds the device idles before each leg (a probe of whether a leg's time "
                         "depends on the load before it; 0: none)")
@@ -1697,10 +1700,10 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
     # the host-path leg first, on a device nothing else has touched yet
     # (measured after the 250 GB of bench buffers were freed it ran at 28 GB/s
     # instead of 46 for Large records)
-    host_path = None if args.no_host_path else host_path_leg(
+    host_path = None if args.no_host_path or args.host_path_at != "first" else host_path_leg(
         _Estimate(args, rank, world), args, local, world, gather_max, all_ok)
     legs = None
-    if args.legs_first:
+    if args.legs_at == "first":
         legs = run_legs(args, rank, local, world, dist, barrier, gather_max, all_ok)
     gc.collect()
     torch.cuda.empty_cache()
@@ -1763,10 +1766,16 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
         scatter = scatter_leg(arena, off, dist, world, all_ok, gpu_parse_check(local),
                               torch.cuda.synchronize)
     bench.release()
+    if args.legs_at == "after_main":
+        legs = run_legs(args, rank, local, world, dist, barrier, gather_max, all_ok)
     decode = None if args.no_decode_legs else decode_legs(bench, args, world, barrier, gather_max,
                                                           all_ok)
-    if not args.legs_first:
+    if args.legs_at == "end":
         legs = run_legs(args, rank, local, world, dist, barrier, gather_max, all_ok)
+    if not args.no_host_path and args.host_path_at == "end":
+        gc.collect()
+        torch.cuda.empty_cache()
+        host_path = host_path_leg(_Estimate(args, rank, world), args, local, world, gather_max, all_ok)
     if rank != 0:
         return None
     if decode is not None and decode.get("materialising") is not None:  # the copy's achievable rate too
@@ -1862,7 +1871,9 @@ def encdec_mode(args, rank, local, world, dist, barrier, gather_max, all_ok):
         "verified_scope": None if ok_all is None else Bench.VERIFIED_SCOPE,
         "decode": decode,
         "legs": legs,
-        "legs_order": "before the main line" if args.legs_first else "after the main line and the decode legs",
+        "legs_order": {"first": "before the main line", "after_main": "after the main line, before the decode legs",
+                       "end": "after the main line and the decode legs"}[args.legs_at],
+        "host_path_order": "before everything" if args.host_path_at == "first" else "after everything",
         "host_path": host_path,
         "scatter": scatter,
     }
