@@ -70,6 +70,10 @@ def test_default_line_legs():
     # only, XLarge encode + decode of 1/16 the records (64 K) + its zero copy
     assert bench.LEG_SHAPES == {"small": ("small", False, 1, False), "mixed_encode": ("mixed", True, 1, False),
                                 "medium": ("medium", False, 1, False), "xlarge": ("xlarge", False, 1 / 16, True)}
+    # the order: host path first (a fresh device), the legs right after the
+    # main line and before the decode legs' 207 GB records arena
+    a = bench.parse_args([])
+    assert (a.host_path_at, a.legs_at) == ("first", "after_main")
 
 
 @pytest.mark.gpu
