@@ -79,15 +79,16 @@ def test_default_line_legs():
 @pytest.mark.gpu
 def test_two_ranks_rehearsal_on_one_gpu():
     """The N > 1 branch of the line (barriers, max over ranks, the all-ranks
-    totals, the scatter leg and its per-rank parse, the decode legs'
-    aggregates) run end to end by two ranks on one GPU (--shared-gpu: gloo
-    instead of RCCL, which refuses two ranks on one device); every rank's
-    records verified. The timing is not a measurement."""
+    totals, the host path on every rank, the scatter leg and its per-rank
+    parse, two shape legs, the decode legs' aggregates) run end to end by two
+    ranks on one GPU (--shared-gpu: gloo instead of RCCL, which refuses two
+    ranks on one device); every rank's records verified. The timing is not a
+    measurement."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     r = _run(["--gpus", "2", "--shared-gpu", "--shape", "small", "--records", "8192", "--steps", "2",
-              "--warmup", "1", "--no-cpu-baseline", "--no-host-path", "--legs", "none"], timeout=300)
+              "--warmup", "1", "--no-cpu-baseline", "--legs", "small,mixed_encode"], timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
@@ -96,3 +97,10 @@ def test_two_ranks_rehearsal_on_one_gpu():
     assert out["config"]["records_per_gpu"] == 8192
     assert out["scatter"]["verified"] is True and out["scatter"]["bytes_sent_by_rank0"] > 0
     assert out["decode"]["verified"] is True and out["decode"]["all_ranks"]["ranks"] == 2
+    # the line's order as the driver runs it: host path first, the shape legs
+    # right after the main line, then the decode legs; every collective of
+    # each leg reached by both ranks
+    assert out["host_path"]["all_ranks"]["ranks"] == 2 and out["host_path"]["rows_match"] is True
+    assert set(out["legs"]) == {"small", "mixed_encode"}
+    assert all(leg["verified"] is True for leg in out["legs"].values())
+    assert out["legs_order"] == "after the main line, before the decode legs"
